@@ -1,0 +1,205 @@
+"""Oracle self-checks (CPU): every op of oracle/unet_ref.py against an
+independent torch-CPU autograd implementation, plus the reference's own
+shape/parameter golden (/root/reference/layers.txt:140-142, restated below)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import unet_ref as R
+
+torch.set_default_dtype(torch.float64)
+
+
+def t(a, grad=False):
+    x = torch.tensor(np.asarray(a, np.float64))
+    x.requires_grad_(grad)
+    return x
+
+
+@pytest.mark.parametrize("k,ci,co", [(3, 3, 8), (3, 16, 8), (1, 8, 3)])
+def test_conv_same_fwd_bwd(k, ci, co):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((2, 9, 7, ci))
+    w = rng.standard_normal((co, k, k, ci))
+    b = rng.standard_normal(co)
+    dz = rng.standard_normal((2, 9, 7, co))
+    y = R.conv2d_same(x, w, b, band=4)
+    dx, dw, db = R.conv2d_same_bwd(x, w, dz, band=4)
+    xt, wt, bt = t(x, True), t(w, True), t(b, True)
+    yt = F.conv2d(xt.permute(0, 3, 1, 2), wt.permute(0, 3, 1, 2), bt, padding=k // 2).permute(0, 2, 3, 1)
+    yt.backward(t(dz))
+    np.testing.assert_allclose(y, yt.detach().numpy(), atol=1e-10)
+    np.testing.assert_allclose(dx, xt.grad.numpy(), atol=1e-10)
+    np.testing.assert_allclose(dw, wt.grad.numpy(), atol=1e-10)
+    np.testing.assert_allclose(db, bt.grad.numpy(), atol=1e-10)
+
+
+def test_tconv_fwd_bwd():
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((2, 3, 5, 6))
+    k = rng.standard_normal((2, 2, 4, 6))  # [a,b,Cout,Cin]
+    b = rng.standard_normal(4)
+    dout = rng.standard_normal((2, 6, 10, 4))
+    y = R.tconv2x2s2(x, k, b)
+    dx, dk, db = R.tconv2x2s2_bwd(x, k, dout)
+    xt, kt, bt = t(x, True), t(k, True), t(b, True)
+    # torch weight for conv_transpose2d: [Cin, Cout, kh, kw]
+    yt = F.conv_transpose2d(xt.permute(0, 3, 1, 2), kt.permute(3, 2, 0, 1), bt, stride=2).permute(0, 2, 3, 1)
+    yt.backward(t(dout))
+    np.testing.assert_allclose(y, yt.detach().numpy(), atol=1e-10)
+    np.testing.assert_allclose(dx, xt.grad.numpy(), atol=1e-10)
+    np.testing.assert_allclose(dk, kt.grad.numpy(), atol=1e-10)
+    np.testing.assert_allclose(db, bt.grad.numpy(), atol=1e-10)
+
+
+def test_maxpool_fwd_bwd_and_tie_rule():
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal((2, 6, 8, 5))
+    y, idx = R.maxpool2x2(x)
+    xt = t(x, True)
+    yt = F.max_pool2d(xt.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    np.testing.assert_allclose(y, yt.detach().numpy())
+    dy = rng.standard_normal(y.shape)
+    yt.backward(t(dy))
+    np.testing.assert_allclose(R.maxpool2x2_bwd(dy, idx, x.shape), xt.grad.numpy())
+    # ties: all-equal window -> gradient to (0,0); tie between (0,1),(1,0) -> (0,1)
+    z = np.zeros((1, 2, 2, 2))
+    z[0, 0, 1, 1] = z[0, 1, 0, 1] = 5.0
+    _, idz = R.maxpool2x2(z)
+    assert idz[0, 0, 0, 0] == 0 and idz[0, 0, 0, 1] == 1
+    g = R.maxpool2x2_bwd(np.ones((1, 1, 1, 2)), idz, z.shape)
+    assert g[0, 0, 0, 0] == 1 and g[0, 0, 1, 1] == 1 and g.sum() == 2
+
+
+def test_bn_train_fwd_bwd():
+    rng = np.random.default_rng(3)
+    r = np.maximum(rng.standard_normal((4, 5, 3, 6)), 0)
+    g = rng.standard_normal(6)
+    b = rng.standard_normal(6)
+    dy = rng.standard_normal(r.shape)
+    y, m, v = R.bn_train_fwd(r, g, b)
+    dr, dg, db = R.bn_train_bwd(dy, r, g, m, v)
+    rt, gt, bt = t(r, True), t(g, True), t(b, True)
+    yt = F.batch_norm(rt.reshape(-1, 6), None, None, gt, bt, training=True, eps=R.BN_EPS).reshape(r.shape)
+    yt.backward(t(dy))
+    np.testing.assert_allclose(y, yt.detach().numpy(), atol=1e-10)
+    np.testing.assert_allclose(dr, rt.grad.numpy(), atol=1e-10)
+    np.testing.assert_allclose(dg, gt.grad.numpy(), atol=1e-10)
+    np.testing.assert_allclose(db, bt.grad.numpy(), atol=1e-10)
+
+
+def test_head_loss_grad_and_rmsprop():
+    rng = np.random.default_rng(4)
+    z = rng.standard_normal((2, 3, 4, 3))
+    tg = rng.uniform(size=z.shape)
+    zt = t(z, True)
+    loss = F.mse_loss(torch.sigmoid(zt), t(tg))
+    loss.backward()
+    yh = R.sigmoid(z)
+    assert abs(R.mse(yh, tg) - loss.item()) < 1e-12
+    np.testing.assert_allclose(R.mse_grad_z(yh, tg), zt.grad.numpy(), atol=1e-12)
+    # RMSprop: torch RMSprop(alpha=rho, eps) adds eps outside the sqrt like Keras
+    p = rng.standard_normal(10)
+    gr = rng.standard_normal(10)
+    pt = t(p, True)
+    opt = torch.optim.RMSprop([pt], lr=R.RMS_LR, alpha=R.RMS_RHO, eps=R.RMS_EPS)
+    pt.grad = t(gr)
+    opt.step()
+    pn, _ = R.rmsprop(p, gr, np.zeros(10))
+    np.testing.assert_allclose(pn, pt.detach().numpy(), atol=1e-12)
+
+
+def test_dropout_hash_stats_and_determinism():
+    k1 = R.dropout_keep(7, 4, 100000)
+    k2 = R.dropout_keep(7, 4, 100000)
+    assert (k1 == k2).all()
+    assert abs(k1.mean() - 0.5) < 0.01
+    assert (R.dropout_keep(7, 4, 1000, start=500) == k1[500:1500]).all()
+    assert (R.dropout_keep(8, 4, 1000) != k1[:1000]).any()
+
+
+def test_param_counts_match_layers_txt():
+    """/root/reference/layers.txt:140-142: Total 11,166,819; trainable 11,159,011;
+    non-trainable 7,808."""
+    P = R.init_unet_params(0)
+    total = sum(v.size for v in P.values())
+    nontrain = sum(v.size for k, v in P.items() if "moving" in k)
+    assert total == 11_166_819
+    assert nontrain == 7_808
+    assert total - nontrain == 11_159_011
+    # per-layer counts quoted in layers.txt
+    assert P["conv2d_11/kernel"].size + 512 == 3_539_456        # layers.txt:87
+    assert P["conv2d_transpose_1/kernel"].size + 512 == 1_049_088  # layers.txt:78
+    assert P["conv2d_15/kernel"].size + 3 == 195                # layers.txt:138
+
+
+def test_unet_full_grad_vs_torch():
+    """Whole U-Net fwd+bwd (training BN, dropout masks from the shared hash) vs a
+    torch autograd build of the same graph (model.py:204-278)."""
+    rng = np.random.default_rng(5)
+    P = R.init_unet_params(1)
+    net = R.UNetRef(P)
+    x = rng.uniform(size=(2, 16, 16, 3))
+    tg = rng.uniform(size=(2, 16, 16, 3))
+    yh = net.forward(x, training=True, seed=11)
+    loss, acc, grads = net.backward(tg)
+
+    T = {k: t(v, True) for k, v in P.items()}
+
+    def conv(xx, n):
+        w = T[n + "/kernel"]
+        return F.conv2d(xx, w.permute(0, 3, 1, 2), T[n + "/bias"], padding=w.shape[1] // 2)
+
+    def tconv(xx, n):
+        return F.conv_transpose2d(xx, T[n + "/kernel"].permute(3, 2, 0, 1), T[n + "/bias"], stride=2)
+
+    def bnrelu(z, n):
+        bn = R.bn_name_for(n)
+        return F.batch_norm(F.relu(z), None, None, T[bn + "/gamma"], T[bn + "/beta"], training=True, eps=R.BN_EPS)
+
+    def drop(y, layer):
+        keep = R.dropout_keep(11, layer, y.numel()).reshape(y.shape[0], y.shape[2], y.shape[3], y.shape[1])
+        m = torch.tensor(keep.astype(np.float64)).permute(0, 3, 1, 2)
+        return y * m * 2
+
+    cb = lambda xx, n: bnrelu(conv(xx, n), n)
+    tb = lambda xx, n: bnrelu(tconv(xx, n), n)
+    xi = t(x).permute(0, 3, 1, 2)
+    c1 = cb(cb(xi, "conv2d_1"), "conv2d_2")
+    c2 = cb(cb(F.max_pool2d(c1, 2), "conv2d_3"), "conv2d_4")
+    c3 = cb(cb(F.max_pool2d(c2, 2), "conv2d_5"), "conv2d_6")
+    c4 = drop(cb(cb(F.max_pool2d(c3, 2), "conv2d_7"), "conv2d_8"), 4)
+    cr = drop(cb(cb(F.max_pool2d(c4, 2), "conv2d_9"), "conv2d_10"), 10)
+    c6 = cb(torch.cat([c4, tb(cr, "conv2d_transpose_1")], 1), "conv2d_11")
+    c7 = cb(torch.cat([c3, tb(c6, "conv2d_transpose_2")], 1), "conv2d_12")
+    c8 = cb(torch.cat([c2, tb(c7, "conv2d_transpose_3")], 1), "conv2d_13")
+    c9 = cb(torch.cat([c1, tb(c8, "conv2d_transpose_4")], 1), "conv2d_14")
+    out = torch.sigmoid(conv(c9, "conv2d_15")).permute(0, 2, 3, 1)
+    lt = F.mse_loss(out, t(tg))
+    lt.backward()
+    np.testing.assert_allclose(yh, out.detach().numpy(), atol=1e-10)
+    assert abs(loss - lt.item()) < 1e-12
+    for k, g in grads.items():
+        np.testing.assert_allclose(g, T[k].grad.numpy(), atol=1e-9, rtol=1e-7, err_msg=k)
+    assert len(grads) == 74  # 19 kernels + 19 biases + 18 gammas + 18 betas
+
+
+def test_tiny_net_grad_vs_torch():
+    rng = np.random.default_rng(6)
+    P = R.init_tiny_params(0)
+    net = R.TinyNetRef(P)
+    x = rng.uniform(size=(1, 12, 12, 3))
+    tg = rng.uniform(size=(1, 12, 12, 3))
+    net.forward(x)
+    loss, _, g = net.backward(tg)
+    T = {k: t(v, True) for k, v in P.items()}
+    h = t(x).permute(0, 3, 1, 2)
+    for n, act in (("conv2d_1", F.relu), ("conv2d_2", F.relu), ("conv2d_3", torch.sigmoid)):
+        w = T[n + "/kernel"]
+        h = act(F.conv2d(h, w.permute(0, 3, 1, 2), T[n + "/bias"], padding=w.shape[1] // 2))
+    lt = F.mse_loss(h.permute(0, 2, 3, 1), t(tg))
+    lt.backward()
+    assert abs(loss - lt.item()) < 1e-12
+    for k in g:
+        np.testing.assert_allclose(g[k], T[k].grad.numpy(), atol=1e-10, err_msg=k)
