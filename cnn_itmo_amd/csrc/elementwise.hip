@@ -1,0 +1,848 @@
+// HBM-bound kernels of the U-Net step: BatchNormalization (train/infer, fwd/bwd),
+// ReLU gradient, Dropout, MaxPooling2D fwd/bwd, the sigmoid head with MSE loss
+// and 'accuracy', RMSprop, weight preparation, first-layer packing and the
+// deterministic column reductions.  All accesses are 16-byte NHWC vectors;
+// every reduction writes per-block partial rows that a fixed-order fp64 pass
+// folds, so results are bitwise reproducible run to run.
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+
+#include "common.h"
+
+// ----------------------------------------------------------------------------
+// Error plumbing (thread-local message for cnnitmo_last_error).
+// ----------------------------------------------------------------------------
+static thread_local char g_err[512];
+void cnnitmo_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+int cnnitmo_check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    cnnitmo_set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return CNNITMO_ELAUNCH;
+  }
+  return CNNITMO_OK;
+}
+extern "C" const char* cnnitmo_last_error(void) { return g_err; }
+extern "C" int cnnitmo_version(void) { return 1; }
+
+static inline int grid_for(long work, int per_block = 256, int cap = 8192) {
+  long b = (work + per_block - 1) / per_block;
+  return (int)std::max(1L, std::min<long>(b, cap));
+}
+
+// ----------------------------------------------------------------------------
+// Column reduction: part [rows][cols] fp32 -> ws [G][cols] fp64 (stage 1).
+// ----------------------------------------------------------------------------
+static constexpr int RED_GMAX = 1024;  // stage-1 row groups (max)
+static inline int red_groups(long rows) { return (int)std::max(1L, std::min<long>(RED_GMAX, rows / 16)); }
+
+// grid (ceil(cols/64), G); block = 64 columns x 4 row lanes; fixed-order fp64 sums.
+__global__ void colsum_stage1(const float* __restrict__ part, long rows, int cols,
+                              double* __restrict__ ws) {
+  const int G = gridDim.y, g = blockIdx.y;
+  const long per = (rows + G - 1) / G;
+  const long r0 = (long)g * per, r1 = std::min(rows, r0 + per);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0;
+  if (c < cols)
+    for (long r = r0 + rl; r < r1; r += 4) s += part[(size_t)r * cols + c];
+  __shared__ double red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (rl == 0 && c < cols)
+    ws[(size_t)g * cols + c] = ((red[cl] + red[cl + 64]) + red[cl + 128]) + red[cl + 192];
+}
+
+static int colsum_stage1_launch(const float* part, long rows, int cols, void* ws, hipStream_t s) {
+  const int G = red_groups(rows);
+  hipLaunchKernelGGL(colsum_stage1, dim3((cols + 63) / 64, G), dim3(256), 0, s, part, rows, cols,
+                     (double*)ws);
+  return G;
+}
+
+__device__ __forceinline__ double fold(const double* ws, int G, int cols, int col) {
+  double s = 0.0;
+  for (int g = 0; g < G; ++g) s += ws[(size_t)g * cols + col];
+  return s;
+}
+
+extern "C" size_t cnnitmo_reduce_workspace_bytes(long rows, int cols) {
+  return (size_t)red_groups(rows) * cols * sizeof(double);
+}
+
+__global__ void colsum_final(const double* __restrict__ ws, int G, int cols, int groups,
+                             float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int C = cols / groups;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int gr = 0; gr < groups; ++gr) s += fold(ws, G, cols, gr * C + c);
+  out[c] = (float)s;
+}
+
+extern "C" int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* out,
+                              void* workspace, void* stream) {
+  CNN_REQUIRE(rows > 0 && cols > 0 && groups > 0 && cols % groups == 0, "colsum: bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  const int G = colsum_stage1_launch(part, rows, cols, workspace, s);
+  const int C = cols / groups;
+  hipLaunchKernelGGL(colsum_final, dim3((C + 255) / 256), dim3(256), 0, s,
+                     (const double*)workspace, G, cols, groups, out);
+  return cnnitmo_check_launch("colsum");
+}
+
+// ----------------------------------------------------------------------------
+// BatchNormalization forward (training) finalize -- model.py:196,200.
+// stat_part [rows][2][groups*C]: (sum r, sum r^2) per GEMM column.
+// ----------------------------------------------------------------------------
+__global__ void bn_fwd_final_kernel(const double* __restrict__ ws, int G, int C, int groups,
+                                    double count, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, float* mm, float* mv,
+                                    float momentum, float eps, float* scale, float* shift,
+                                    float* smean, float* sinv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int cols = 2 * groups * C;
+  double s1 = 0.0, s2 = 0.0;
+  for (int gr = 0; gr < groups; ++gr) {
+    s1 += fold(ws, G, cols, gr * C + c);
+    s2 += fold(ws, G, cols, groups * C + gr * C + c);
+  }
+  const double mean = s1 / count;
+  const double var = fmax(s2 / count - mean * mean, 0.0);  // biased (tf.nn.moments)
+  const double inv = 1.0 / sqrt(var + (double)eps);
+  const double sc = (double)gamma[c] * inv;
+  scale[c] = (float)sc;
+  shift[c] = (float)((double)beta[c] - mean * sc);
+  smean[c] = (float)mean;
+  sinv[c] = (float)inv;
+  if (mm && mv) {
+    // Keras 2.2.x: var *= n / (n - (1 + eps)); moving = moving*m + v*(1-m)
+    const double var_u = var * (count / (count - (1.0 + (double)eps)));
+    mm[c] = (float)((double)mm[c] * momentum + mean * (1.0 - momentum));
+    mv[c] = (float)((double)mv[c] * momentum + var_u * (1.0 - momentum));
+  }
+}
+
+extern "C" int cnnitmo_bn_fwd_finalize(const float* stat_part, long rows, int c, int groups,
+                                       double count, const float* gamma, const float* beta,
+                                       float* moving_mean, float* moving_var, float momentum,
+                                       float eps, float* scale, float* shift, float* save_mean,
+                                       float* save_invstd, void* workspace, void* stream) {
+  CNN_REQUIRE(rows > 0 && c > 0 && groups >= 1 && count > 1.0, "bn_fwd_finalize: bad sizes");
+  hipStream_t s = (hipStream_t)stream;
+  const int G = colsum_stage1_launch(stat_part, rows, 2 * groups * c, workspace, s);
+  hipLaunchKernelGGL(bn_fwd_final_kernel, dim3((c + 255) / 256), dim3(256), 0, s,
+                     (const double*)workspace, G, c, groups, count, gamma, beta, moving_mean,
+                     moving_var, momentum, eps, scale, shift, save_mean, save_invstd);
+  return cnnitmo_check_launch("bn_fwd_finalize");
+}
+
+__global__ void bn_infer_kernel(int C, const float* g, const float* b, const float* mm,
+                                const float* mv, float eps, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float sc = g[c] / sqrtf(mv[c] + eps);
+  scale[c] = sc;
+  shift[c] = b[c] - mm[c] * sc;
+}
+
+extern "C" int cnnitmo_bn_infer_coeffs(int c, const float* gamma, const float* beta,
+                                       const float* mmean, const float* mvar, float eps,
+                                       float* scale, float* shift, void* stream) {
+  hipLaunchKernelGGL(bn_infer_kernel, dim3((c + 255) / 256), dim3(256), 0, (hipStream_t)stream, c,
+                     gamma, beta, mmean, mvar, eps, scale, shift);
+  return cnnitmo_check_launch("bn_infer_coeffs");
+}
+
+// y view = r*scale + shift [+ Dropout(0.5)].  One thread = one 16-byte vector.
+template <typename T>
+__global__ void bn_apply_kernel(const T* __restrict__ r, long P, int C, const float* __restrict__ sc,
+                                const float* __restrict__ sh, T* __restrict__ y, long y_ld, int y_off,
+                                int drop, uint64_t dbase) {
+  constexpr int VE = Vec16<T>::N;
+  const int cv = C / VE;
+  const long total = P * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long p = i / cv;
+    const int c0 = (int)(i - p * cv) * VE;
+    float v[VE];
+    Pack16<T>::load(r + (size_t)p * C + c0, v);
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      float o = v[e] * sc[c0 + e] + sh[c0 + e];
+      if (drop) o = dropout_keep(dbase, (uint64_t)p * C + c0 + e) ? o * 2.f : 0.f;
+      v[e] = o;
+    }
+    Pack16<T>::store(y + (size_t)p * y_ld + y_off + c0, v);
+  }
+}
+
+extern "C" int cnnitmo_bn_apply(int dtype, const void* r, long p, int c, const float* scale,
+                                const float* shift, void* y, int y_ld, int y_off, int flags,
+                                uint64_t drop_seed, int drop_layer, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int drop = (flags & CNNITMO_DROPOUT) ? 1 : 0;
+  const uint64_t base = dropout_base(drop_seed, (uint64_t)drop_layer);
+  CNN_REQUIRE(c % 8 == 0 && y_ld % 8 == 0 && y_off % 8 == 0, "bn_apply: channels must be multiples of 8");
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(grid_for(p * c / 8)), dim3(256), 0, s,
+                       (const bf16*)r, p, c, scale, shift, (bf16*)y, (long)y_ld, y_off, drop, base);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_for(p * c / 4)), dim3(256), 0, s,
+                       (const float*)r, p, c, scale, shift, (float*)y, (long)y_ld, y_off, drop, base);
+  return cnnitmo_check_launch("bn_apply");
+}
+
+// ----------------------------------------------------------------------------
+// BN backward.  Thread layout: TPP = C/VE threads per pixel row, ROWS = 256/TPP
+// pixel rows per block iteration; each thread keeps VE channels of sums.
+// ----------------------------------------------------------------------------
+static constexpr int BWD_BLOCKS = 1024;
+
+extern "C" int cnnitmo_bn_bwd_rows(long p, int c) {
+  (void)c;
+  return (int)std::max<long>(1, std::min<long>(BWD_BLOCKS, (p + 7) / 8));
+}
+
+template <typename T>
+__device__ __forceinline__ void load_dy(const T* dy, long dy_ld, int dy_off, long p, int C, int c0,
+                                        int drop, uint64_t dbase, float* v) {
+  constexpr int VE = Vec16<T>::N;
+  Pack16<T>::load(dy + (size_t)p * dy_ld + dy_off + c0, v);
+  if (drop) {
+#pragma unroll
+    for (int e = 0; e < VE; ++e)
+      v[e] = dropout_keep(dbase, (uint64_t)p * C + c0 + e) ? v[e] * 2.f : 0.f;
+  }
+}
+
+// Block-level reduction of per-thread [VE][NS] sums into part[blockIdx.x][NS][C].
+template <int VE, int NS>
+__device__ void block_reduce_rows(float (&acc)[NS][VE], int C, float* __restrict__ part) {
+  __shared__ float red[256 * VE * NS];
+  const int tpp = C / VE;
+  const int rows = 256 / tpp;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int e = 0; e < VE; ++e) red[(k * 256 + tid) * VE + e] = acc[k][e];
+  __syncthreads();
+  for (int idx = tid; idx < NS * C; idx += 256) {
+    const int k = idx / C, c = idx - k * C;
+    const int cv = c / VE, e = c - cv * VE;
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += red[(k * 256 + r * tpp + cv) * VE + e];
+    part[((size_t)blockIdx.x * NS + k) * C + c] = s;
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(const T* __restrict__ dy, long dy_ld, int dy_off,
+                                     const T* __restrict__ r, long P, int C,
+                                     const float* __restrict__ mean, const float* __restrict__ inv,
+                                     int drop, uint64_t dbase, float* __restrict__ part) {
+  constexpr int VE = Vec16<T>::N;
+  const int tpp = C / VE, rows = 256 / tpp;
+  const int tid = threadIdx.x;
+  const int row = tid / tpp, cv = tid - row * tpp, c0 = cv * VE;
+  float acc[2][VE];
+#pragma unroll
+  for (int e = 0; e < VE; ++e) acc[0][e] = acc[1][e] = 0.f;
+  float mu[VE], is[VE];
+#pragma unroll
+  for (int e = 0; e < VE; ++e) {
+    mu[e] = row < rows ? mean[c0 + e] : 0.f;
+    is[e] = row < rows ? inv[c0 + e] : 0.f;
+  }
+  if (row < rows) {
+    for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
+      float g[VE], rv[VE];
+      load_dy<T>(dy, dy_ld, dy_off, p, C, c0, drop, dbase, g);
+      Pack16<T>::load(r + (size_t)p * C + c0, rv);
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        acc[0][e] += g[e];
+        acc[1][e] += g[e] * (rv[e] - mu[e]) * is[e];
+      }
+    }
+  }
+  block_reduce_rows<VE, 2>(acc, C, part);
+}
+
+extern "C" int cnnitmo_bn_bwd_reduce(int dtype, const void* dy, int dy_ld, int dy_off,
+                                     const void* r, long p, int c, const float* mean,
+                                     const float* invstd, int flags, uint64_t drop_seed,
+                                     int drop_layer, float* part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int G = cnnitmo_bn_bwd_rows(p, c);
+  const int drop = (flags & CNNITMO_DROPOUT) ? 1 : 0;
+  const uint64_t base = dropout_base(drop_seed, (uint64_t)drop_layer);
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % VE == 0 && c / VE <= 256 && dy_ld % VE == 0 && dy_off % VE == 0,
+              "bn_bwd_reduce: unsupported channel count %d", c);
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dy,
+                       (long)dy_ld, dy_off, (const bf16*)r, p, c, mean, invstd, drop, base, part);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dy,
+                       (long)dy_ld, dy_off, (const float*)r, p, c, mean, invstd, drop, base, part);
+  return cnnitmo_check_launch("bn_bwd_reduce");
+}
+
+// coef [3][C]: dz = [r>0] * (a*dy - b*r + e)
+__global__ void bn_bwd_final_kernel(const double* __restrict__ ws, int G, int C, double count,
+                                    const float* __restrict__ gamma, const float* __restrict__ mean,
+                                    const float* __restrict__ inv, float* dgamma, float* dbeta,
+                                    float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double sdy = fold(ws, G, 2 * C, c), sdyr = fold(ws, G, 2 * C, C + c);
+  if (dgamma) dgamma[c] = (float)sdyr;
+  if (dbeta) dbeta[c] = (float)sdy;
+  const double a = (double)gamma[c] * inv[c];
+  const double b = a * inv[c] * sdyr / count;
+  const double e = b * mean[c] - a * sdy / count;
+  coef[c] = (float)a;
+  coef[C + c] = (float)b;
+  coef[2 * C + c] = (float)e;
+}
+
+extern "C" int cnnitmo_bn_bwd_finalize(const float* part, long rows, int c, double count,
+                                       const float* gamma, const float* mean, const float* invstd,
+                                       float* dgamma, float* dbeta, float* coef, void* workspace,
+                                       void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int G = colsum_stage1_launch(part, rows, 2 * c, workspace, s);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((c + 255) / 256), dim3(256), 0, s,
+                     (const double*)workspace, G, c, count, gamma, mean, invstd, dgamma, dbeta, coef);
+  return cnnitmo_check_launch("bn_bwd_finalize");
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, long dy_ld, int dy_off,
+                                    const T* __restrict__ r, long P, int C,
+                                    const float* __restrict__ coef, int nobn, int drop,
+                                    uint64_t dbase, T* __restrict__ dz, float* __restrict__ part) {
+  constexpr int VE = Vec16<T>::N;
+  const int tpp = C / VE, rows = 256 / tpp;
+  const int tid = threadIdx.x;
+  const int row = tid / tpp, cv = tid - row * tpp, c0 = cv * VE;
+  float acc[1][VE];
+  float ca[VE], cb[VE], ce[VE];
+#pragma unroll
+  for (int e = 0; e < VE; ++e) {
+    acc[0][e] = 0.f;
+    const bool ok = row < rows && !nobn;
+    ca[e] = ok ? coef[c0 + e] : 1.f;
+    cb[e] = ok ? coef[C + c0 + e] : 0.f;
+    ce[e] = ok ? coef[2 * C + c0 + e] : 0.f;
+  }
+  if (row < rows) {
+    for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
+      float g[VE], rv[VE];
+      load_dy<T>(dy, dy_ld, dy_off, p, C, c0, drop, dbase, g);
+      Pack16<T>::load(r + (size_t)p * C + c0, rv);
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        const float d = rv[e] > 0.f ? (ca[e] * g[e] - cb[e] * rv[e] + ce[e]) : 0.f;
+        g[e] = d;
+      }
+      Pack16<T>::store(dz + (size_t)p * C + c0, g);
+      // bias gradient from the stored (rounded) dz, as the weight gradient sees it
+#pragma unroll
+      for (int e = 0; e < VE; ++e) acc[0][e] += to_f32(from_f32<T>(g[e]));
+    }
+  }
+  block_reduce_rows<VE, 1>(acc, C, part);
+}
+
+extern "C" int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off,
+                                    const void* r, long p, int c, const float* coef, int flags,
+                                    uint64_t drop_seed, int drop_layer, void* dz, float* part,
+                                    void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int G = cnnitmo_bn_bwd_rows(p, c);
+  const int drop = (flags & CNNITMO_DROPOUT) ? 1 : 0;
+  const int nobn = (flags & CNNITMO_NO_BN) ? 1 : 0;
+  const uint64_t base = dropout_base(drop_seed, (uint64_t)drop_layer);
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % VE == 0 && c / VE <= 256 && dy_ld % VE == 0 && dy_off % VE == 0,
+              "bn_bwd_apply: unsupported channel count %d", c);
+  CNN_REQUIRE(nobn || coef, "bn_bwd_apply: missing coefficients");
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dy,
+                       (long)dy_ld, dy_off, (const bf16*)r, p, c, coef, nobn, drop, base, (bf16*)dz, part);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dy,
+                       (long)dy_ld, dy_off, (const float*)r, p, c, coef, nobn, drop, base, (float*)dz,
+                       part);
+  return cnnitmo_check_launch("bn_bwd_apply");
+}
+
+// ----------------------------------------------------------------------------
+// MaxPooling2D 2x2 s2 -- model.py:210,215,220,227.  Tie rule: first maximum in
+// window order (0,0),(0,1),(1,0),(1,1) (strict '>' scan), shared with the oracle.
+// ----------------------------------------------------------------------------
+template <typename T>
+__global__ void maxpool_fwd_kernel(const T* __restrict__ x, long x_ld, int x_off, int N, int H,
+                                   int W, int C, T* __restrict__ y, uint8_t* __restrict__ idx) {
+  constexpr int VE = Vec16<T>::N;
+  const int Ho = H / 2, Wo = W / 2, cv = C / VE;
+  const long total = (long)N * Ho * Wo * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long po = i / cv;
+    const int c0 = (int)(i - po * cv) * VE;
+    const int n = (int)(po / ((long)Ho * Wo));
+    const int rem = (int)(po - (long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    float best[VE];
+    uint8_t arg[VE];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const long pin = ((long)n * H + 2 * ho + (k >> 1)) * W + 2 * wo + (k & 1);
+      float v[VE];
+      Pack16<T>::load(x + (size_t)pin * x_ld + x_off + c0, v);
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        if (k == 0 || v[e] > best[e]) {
+          best[e] = v[e];
+          arg[e] = (uint8_t)k;
+        }
+      }
+    }
+    Pack16<T>::store(y + (size_t)po * C + c0, best);
+    if constexpr (VE == 8) {
+      uint2 a;
+      a.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
+      a.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | ((uint32_t)arg[7] << 24);
+      *reinterpret_cast<uint2*>(idx + (size_t)po * C + c0) = a;
+    } else {
+      *reinterpret_cast<uint32_t*>(idx + (size_t)po * C + c0) =
+          arg[0] | (arg[1] << 8) | (arg[2] << 16) | ((uint32_t)arg[3] << 24);
+    }
+  }
+}
+
+template <typename T>
+__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, int N,
+                                   int H, int W, int C, T* __restrict__ dx, long dx_ld, int dx_off) {
+  constexpr int VE = Vec16<T>::N;
+  const int Ho = H / 2, Wo = W / 2, cv = C / VE;
+  const long total = (long)N * Ho * Wo * cv;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long po = i / cv;
+    const int c0 = (int)(i - po * cv) * VE;
+    const int n = (int)(po / ((long)Ho * Wo));
+    const int rem = (int)(po - (long)n * Ho * Wo);
+    const int ho = rem / Wo, wo = rem - ho * Wo;
+    float g[VE];
+    Pack16<T>::load(dy + (size_t)po * C + c0, g);
+    uint8_t arg[VE];
+#pragma unroll
+    for (int e = 0; e < VE; ++e) arg[e] = idx[(size_t)po * C + c0 + e];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bool any = false;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) any |= arg[e] == k;
+      if (!any) continue;
+      const long pin = ((long)n * H + 2 * ho + (k >> 1)) * W + 2 * wo + (k & 1);
+      T* q = dx + (size_t)pin * dx_ld + dx_off + c0;
+      float v[VE];
+      Pack16<T>::load(q, v);
+#pragma unroll
+      for (int e = 0; e < VE; ++e)
+        if (arg[e] == k) v[e] += g[e];
+      Pack16<T>::store(q, v);
+    }
+  }
+}
+
+extern "C" int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h,
+                                      int w, int c, void* y, uint8_t* idx, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  CNN_REQUIRE(c % 8 == 0 && x_ld % 8 == 0 && x_off % 8 == 0, "maxpool_fwd: channels must be multiples of 8");
+  const long work = (long)n * (h / 2) * (w / 2) * c;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(grid_for(work / 8)), dim3(256), 0, s,
+                       (const bf16*)x, (long)x_ld, x_off, n, h, w, c, (bf16*)y, idx);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid_for(work / 4)), dim3(256), 0, s,
+                       (const float*)x, (long)x_ld, x_off, n, h, w, c, (float*)y, idx);
+  return cnnitmo_check_launch("maxpool_fwd");
+}
+
+extern "C" int cnnitmo_maxpool2x2_bwd(int dtype, const void* dy, const uint8_t* idx, int n, int h,
+                                      int w, int c, void* dx, int dx_ld, int dx_off, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  CNN_REQUIRE(c % 8 == 0 && dx_ld % 8 == 0 && dx_off % 8 == 0, "maxpool_bwd: channels must be multiples of 8");
+  const long work = (long)n * (h / 2) * (w / 2) * c;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(grid_for(work / 8)), dim3(256), 0, s,
+                       (const bf16*)dy, idx, n, h, w, c, (bf16*)dx, (long)dx_ld, dx_off);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid_for(work / 4)), dim3(256), 0, s,
+                       (const float*)dy, idx, n, h, w, c, (float*)dx, (long)dx_ld, dx_off);
+  return cnnitmo_check_launch("maxpool_bwd");
+}
+
+// ----------------------------------------------------------------------------
+// Head: Conv2D(3, 1, activation='sigmoid') + MSE + categorical accuracy
+// (model.py:276,281).  LPP = cin/VE lanes share one pixel.
+// part row layout: [loss, correct, db0..2, dW[3][cin]]
+// ----------------------------------------------------------------------------
+static constexpr int HEAD_BLOCKS = 1024;
+extern "C" int cnnitmo_head_rows(long p) {
+  return (int)std::max<long>(1, std::min<long>(HEAD_BLOCKS, (p + 31) / 32));
+}
+
+template <typename T, bool BWD>
+__global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W, int cin,
+                            const float* __restrict__ wt, const float* __restrict__ bias,
+                            const float* __restrict__ target, float* __restrict__ yhat,
+                            T* __restrict__ dx, float inv_numel, float* __restrict__ part) {
+  constexpr int VE = Vec16<T>::N;
+  const int lpp = cin / VE;             // lanes per pixel (power of two <= 64)
+  const int ppb = 256 / lpp;            // pixels per block iteration
+  const int tid = threadIdx.x, sub = tid % lpp, slot = tid / lpp;
+  const int c0 = sub * VE;
+  float w[3][VE];
+#pragma unroll
+  for (int o = 0; o < 3; ++o)
+#pragma unroll
+    for (int e = 0; e < VE; ++e) w[o][e] = wt[o * cin + c0 + e];
+  const float b0 = bias[0], b1 = bias[1], b2 = bias[2];
+  float dwacc[3][VE];
+#pragma unroll
+  for (int o = 0; o < 3; ++o)
+#pragma unroll
+    for (int e = 0; e < VE; ++e) dwacc[o][e] = 0.f;
+  float lsum = 0.f, corr = 0.f, db[3] = {0.f, 0.f, 0.f};
+  const long P = (long)N * H * W;
+  for (long base = (long)blockIdx.x * ppb; base < P; base += (long)gridDim.x * ppb) {
+    const long p = base + slot;
+    const bool inb = p < P;
+    float v[VE];
+    if (inb) Pack16<T>::load(x + (size_t)p * cin + c0, v);
+    else
+#pragma unroll
+      for (int e = 0; e < VE; ++e) v[e] = 0.f;
+    float z[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) s += v[e] * w[o][e];
+      for (int off = lpp >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+      z[o] = s;
+    }
+    z[0] += b0; z[1] += b1; z[2] += b2;
+    float yh[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) yh[o] = 1.f / (1.f + expf(-z[o]));
+    const int n = inb ? (int)(p / ((long)H * W)) : 0;
+    const int rem = inb ? (int)(p - (long)n * H * W) : 0;
+    const int h = rem / W, wc = rem - h * W;
+    const bool valid = inb && h < Hv;
+    const size_t tix = (((size_t)n * Hv + h) * W + wc) * 3;
+    if (!BWD) {
+      if (valid && sub == 0) {
+        yhat[tix + 0] = yh[0];
+        yhat[tix + 1] = yh[1];
+        yhat[tix + 2] = yh[2];
+      }
+      continue;
+    }
+    float dz[3] = {0.f, 0.f, 0.f};
+    if (valid) {
+      const float t0 = target[tix], t1 = target[tix + 1], t2 = target[tix + 2];
+      const float e0 = yh[0] - t0, e1 = yh[1] - t1, e2 = yh[2] - t2;
+      if (sub == 0) {
+        lsum += e0 * e0 + e1 * e1 + e2 * e2;
+        const int at = (t1 > t0) ? ((t2 > t1) ? 2 : 1) : ((t2 > t0) ? 2 : 0);
+        const int ap = (yh[1] > yh[0]) ? ((yh[2] > yh[1]) ? 2 : 1) : ((yh[2] > yh[0]) ? 2 : 0);
+        corr += (at == ap) ? 1.f : 0.f;
+      }
+      dz[0] = 2.f * e0 * yh[0] * (1.f - yh[0]) * inv_numel;
+      dz[1] = 2.f * e1 * yh[1] * (1.f - yh[1]) * inv_numel;
+      dz[2] = 2.f * e2 * yh[2] * (1.f - yh[2]) * inv_numel;
+    }
+    if (sub == 0) {
+      db[0] += dz[0]; db[1] += dz[1]; db[2] += dz[2];
+    }
+    float g[VE];
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      g[e] = dz[0] * w[0][e] + dz[1] * w[1][e] + dz[2] * w[2][e];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) dwacc[o][e] += dz[o] * v[e];
+    }
+    if (inb) Pack16<T>::store(dx + (size_t)p * cin + c0, g);
+  }
+  if (!BWD) return;
+  // reduce: lanes with equal `sub` hold the same channel slice
+  __shared__ float red[256][3 * 8 + 5];
+#pragma unroll
+  for (int o = 0; o < 3; ++o)
+#pragma unroll
+    for (int e = 0; e < VE; ++e) red[tid][o * VE + e] = dwacc[o][e];
+  red[tid][3 * VE + 0] = lsum;
+  red[tid][3 * VE + 1] = corr;
+  red[tid][3 * VE + 2] = db[0];
+  red[tid][3 * VE + 3] = db[1];
+  red[tid][3 * VE + 4] = db[2];
+  __syncthreads();
+  const int ncol = 5 + 3 * cin;
+  float* out = part + (size_t)blockIdx.x * ncol;
+  for (int k = tid; k < ncol; k += 256) {
+    float s = 0.f;
+    if (k < 5) {
+      for (int t = 0; t < 256; t += lpp) s += red[t][3 * VE + k];
+    } else {
+      const int q = k - 5, o = q / cin, c = q - o * cin;
+      const int sb = c / VE, e = c - sb * VE;
+      for (int t = sb; t < 256; t += lpp) s += red[t][o * VE + e];
+    }
+    out[k] = s;
+  }
+}
+
+extern "C" int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
+                                const float* wt, const float* b, float* yhat, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
+              "head: cin/%d must be a power of two <= 64", VE);
+  const long P = (long)n * h * w;
+  const int G = cnnitmo_head_rows(P);
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL((head_kernel<bf16, false>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
+                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr);
+  else
+    hipLaunchKernelGGL((head_kernel<float, false>), dim3(G), dim3(256), 0, s, (const float*)x, n, h,
+                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr);
+  return cnnitmo_check_launch("head_fwd");
+}
+
+extern "C" int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w,
+                                    int cin, const float* wt, const float* b, const float* target,
+                                    void* dx, float* part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
+              "head: cin/%d must be a power of two <= 64", VE);
+  const long P = (long)n * h * w;
+  const int G = cnnitmo_head_rows(P);
+  const float inv_numel = (float)(1.0 / ((double)n * h_valid * w * 3));
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL((head_kernel<bf16, true>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
+                       h_valid, w, cin, wt, b, target, nullptr, (bf16*)dx, inv_numel, part);
+  else
+    hipLaunchKernelGGL((head_kernel<float, true>), dim3(G), dim3(256), 0, s, (const float*)x, n, h,
+                       h_valid, w, cin, wt, b, target, nullptr, (float*)dx, inv_numel, part);
+  return cnnitmo_check_launch("head_fwd_bwd");
+}
+
+__global__ void head_final_kernel(const double* __restrict__ ws, int G, int cin, double numel,
+                                  float* loss_acc, float* dw, float* db) {
+  const int ncol = 5 + 3 * cin;
+  for (int k = threadIdx.x; k < ncol; k += blockDim.x) {
+    const double s = fold(ws, G, ncol, k);
+    if (k == 0) loss_acc[0] = (float)(s / numel);
+    else if (k == 1) loss_acc[1] = (float)(s / (numel / 3.0));
+    else if (k < 5) db[k - 2] = (float)s;
+    else dw[k - 5] = (float)s;
+  }
+}
+
+extern "C" int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
+                                     float* loss_acc, float* dw, float* db, void* workspace,
+                                     void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int G = colsum_stage1_launch(part, rows, 5 + 3 * cin, workspace, s);
+  hipLaunchKernelGGL(head_final_kernel, dim3(1), dim3(256), 0, s, (const double*)workspace, G, cin,
+                     numel, loss_acc, dw, db);
+  return cnnitmo_check_launch("head_finalize");
+}
+
+// ----------------------------------------------------------------------------
+// RMSprop (Keras 2.2 defaults; eps outside the sqrt) over one flat buffer.
+// ----------------------------------------------------------------------------
+__global__ void rmsprop_kernel(float* __restrict__ p, const float* __restrict__ g,
+                               float* __restrict__ a, long n, float lr, float rho, float eps,
+                               float gs) {
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4;
+       i += (long)gridDim.x * blockDim.x) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 av = reinterpret_cast<float4*>(a)[i];
+    float* pp = &pv.x;
+    const float* gg = &gv.x;
+    float* aa = &av.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float gr = gg[e] * gs;
+      aa[e] = rho * aa[e] + (1.f - rho) * gr * gr;
+      pp[e] -= lr * gr / (sqrtf(aa[e]) + eps);
+    }
+    reinterpret_cast<float4*>(p)[i] = pv;
+    reinterpret_cast<float4*>(a)[i] = av;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n;
+       i += (long)gridDim.x * blockDim.x) {
+    const float gr = g[i] * gs;
+    a[i] = rho * a[i] + (1.f - rho) * gr * gr;
+    p[i] -= lr * gr / (sqrtf(a[i]) + eps);
+  }
+}
+
+extern "C" int cnnitmo_rmsprop(float* p, const float* g, float* a, long n, float lr, float rho,
+                               float eps, float grad_scale, void* stream) {
+  CNN_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)a) % 16 == 0, "rmsprop: buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(rmsprop_kernel, dim3(grid_for(n / 4 + 1, 256, 2048)), dim3(256), 0,
+                     (hipStream_t)stream, p, g, a, n, lr, rho, eps, grad_scale);
+  return cnnitmo_check_launch("rmsprop");
+}
+
+// ----------------------------------------------------------------------------
+// Weight preparation: fp32 master -> dtype copies in the layouts kernels read.
+// ----------------------------------------------------------------------------
+template <typename T>
+__global__ void prep_conv_kernel(const float* __restrict__ w, int cout, int cin, T* __restrict__ wf,
+                                 T* __restrict__ wflip) {
+  const long total = (long)cout * 9 * cin;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cin);
+    const long t = i / cin;
+    const int rs = (int)(t % 9), co = (int)(t / 9);
+    const T v = from_f32<T>(w[i]);
+    wf[i] = v;
+    if (wflip) {  // wflip[ci][2-r][2-s][co] = w[co][r][s][ci]
+      const int r = rs / 3, s = rs % 3;
+      wflip[((long)ci * 9 + (2 - r) * 3 + (2 - s)) * cout + co] = v;
+    }
+  }
+}
+
+template <typename T>
+__global__ void prep_tconv_kernel(const float* __restrict__ k, int cout, int cin, T* __restrict__ kf,
+                                  T* __restrict__ kT) {
+  const long total = 4L * cout * cin;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cin);
+    const long t = i / cin;
+    const int co = (int)(t % cout), tap = (int)(t / cout);
+    const T v = from_f32<T>(k[i]);
+    kf[i] = v;
+    kT[((long)ci * 4 + tap) * cout + co] = v;  // kT[ci][a][b][co]
+  }
+}
+
+template <typename T>
+__global__ void prep_c3_kernel(const float* __restrict__ w, int cout, T* __restrict__ wp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cout * 32) return;
+  const int co = i / 32, k = i % 32;
+  wp[i] = from_f32<T>(k < 27 ? w[co * 27 + k] : 0.f);
+}
+
+extern "C" int cnnitmo_prep_conv3x3_weights(int dtype, const float* w, int cout, int cin,
+                                            void* w_fwd, void* w_flip, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long n = (long)cout * 9 * cin;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(prep_conv_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, w, cout, cin,
+                       (bf16*)w_fwd, (bf16*)w_flip);
+  else
+    hipLaunchKernelGGL(prep_conv_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, w, cout, cin,
+                       (float*)w_fwd, (float*)w_flip);
+  return cnnitmo_check_launch("prep_conv3x3_weights");
+}
+
+extern "C" int cnnitmo_prep_tconv2x2_weights(int dtype, const float* k, int cout, int cin,
+                                             void* k_fwd, void* kT, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long n = 4L * cout * cin;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(prep_tconv_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, k, cout, cin,
+                       (bf16*)k_fwd, (bf16*)kT);
+  else
+    hipLaunchKernelGGL(prep_tconv_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, k, cout, cin,
+                       (float*)k_fwd, (float*)kT);
+  return cnnitmo_check_launch("prep_tconv2x2_weights");
+}
+
+extern "C" int cnnitmo_prep_c3_weights(int dtype, const float* w, int cout, void* w_packed,
+                                       void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(prep_c3_kernel<bf16>, dim3((cout * 32 + 255) / 256), dim3(256), 0, s, w,
+                       cout, (bf16*)w_packed);
+  else
+    hipLaunchKernelGGL(prep_c3_kernel<float>, dim3((cout * 32 + 255) / 256), dim3(256), 0, s, w,
+                       cout, (float*)w_packed);
+  return cnnitmo_check_launch("prep_c3_weights");
+}
+
+// ----------------------------------------------------------------------------
+// First-layer packing: x [n][h_valid][w][3] fp32 -> cols [n][h][w][32] dtype.
+// ----------------------------------------------------------------------------
+template <typename T>
+__global__ void im2col_c3_kernel(const float* __restrict__ x, int N, int Hv, int H, int W,
+                                 T* __restrict__ cols) {
+  constexpr int VE = Vec16<T>::N;
+  constexpr int CV = 32 / VE;  // vectors per pixel
+  const long total = (long)N * H * W * CV;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long p = i / CV;
+    const int k0 = (int)(i - p * CV) * VE;
+    const int n = (int)(p / ((long)H * W));
+    const int rem = (int)(p - (long)n * H * W);
+    const int h = rem / W, w = rem - h * W;
+    float v[VE];
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      const int k = k0 + e;
+      float val = 0.f;
+      if (k < 27) {
+        const int tap = k / 3, c = k - tap * 3;
+        const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+        if (hh >= 0 && hh < Hv && ww >= 0 && ww < W)
+          val = x[(((size_t)n * Hv + hh) * W + ww) * 3 + c];
+      }
+      v[e] = val;
+    }
+    Pack16<T>::store(cols + (size_t)p * 32 + k0, v);
+  }
+}
+
+extern "C" int cnnitmo_im2col_c3(int dtype, const float* x, int n, int h_valid, int h, int w,
+                                 void* cols, void* stream) {
+  CNN_REQUIRE(h_valid <= h, "im2col_c3: h_valid > h");
+  hipStream_t s = (hipStream_t)stream;
+  const long work = (long)n * h * w * 4;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(im2col_c3_kernel<bf16>, dim3(grid_for(work)), dim3(256), 0, s, x, n,
+                       h_valid, h, w, (bf16*)cols);
+  else
+    hipLaunchKernelGGL(im2col_c3_kernel<float>, dim3(grid_for(work * 2)), dim3(256), 0, s, x, n,
+                       h_valid, h, w, (float*)cols);
+  return cnnitmo_check_launch("im2col_c3");
+}

@@ -1,0 +1,206 @@
+"""Thin typed wrappers over the C ABI (include/cnn_itmo.h).
+
+Activations are passed as ``View`` objects: an NHWC channel window
+(buffer, ld, off) of a device buffer -- the zero-copy concatenation of
+model.py:246-261 is just two views of one buffer.  torch supplies device
+memory and the current HIP stream; every FLOP runs in libcnnitmo.so.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+from ._lib import call, query
+
+DTYPES = {"float32": (L.F32, torch.float32), "bfloat16": (L.BF16, torch.bfloat16)}
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+@dataclass
+class View:
+    """Element (p, c) of an [n, h, w, c] activation is buf[p*ld + off + c]."""
+    buf: torch.Tensor
+    n: int
+    h: int
+    w: int
+    c: int
+    ld: int
+    off: int = 0
+
+    @property
+    def p(self):
+        return self.n * self.h * self.w
+
+    @property
+    def ptr(self):
+        return self.buf.data_ptr()
+
+    def tensor(self):
+        """[n, h, w, c] strided torch view (for tests / host copies)."""
+        return self.buf.view(-1)[self.off:].as_strided((self.n, self.h, self.w, self.c),
+                                                       (self.h * self.w * self.ld, self.w * self.ld, self.ld, 1))
+
+
+def new_view(n, h, w, c, dtype, device="cuda"):
+    return View(torch.empty(n * h * w * c, dtype=dtype, device=device), n, h, w, c, c, 0)
+
+
+def workspace(nbytes, device="cuda"):
+    return torch.empty(max(16, int(nbytes)), dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------- convolutions
+def conv3x3_fwd(dt, x: View, wt, bias, out: View, flags=0, aff=None, stats=None):
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_conv3x3_fwd", dt, x.ptr, x.ld, x.off, x.n, x.h, x.w, x.c, ptr(wt), ptr(bias),
+         out.c, out.ptr, out.ld, out.off, flags, ptr(sc), ptr(sh), ptr(stats), stream_ptr())
+
+
+def conv1tap_fwd(dt, cols, k, m, wt, bias, out: View, flags=0, aff=None, stats=None):
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_conv1tap_fwd", dt, ptr(cols), k, m, ptr(wt), ptr(bias), out.c, out.ptr, out.ld,
+         out.off, flags, ptr(sc), ptr(sh), ptr(stats), stream_ptr())
+
+
+def fwd_stat_rows(dt, m, ncols):
+    return query("cnnitmo_fwd_stat_rows", dt, m, ncols)
+
+
+def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx: View):
+    call("cnnitmo_conv3x3_dgrad", dt, ptr(dz), n, h, w, cout, ptr(wflip), cin, dx.ptr, dx.ld, dx.off,
+         stream_ptr())
+
+
+def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0):
+    nbytes = query("cnnitmo_wgrad_workspace_bytes", dt, x.n, x.h, x.w, x.c, cout, ntaps)
+    ws = workspace(nbytes, dz.device)
+    call("cnnitmo_conv_wgrad", dt, ntaps, x.ptr, x.ld, x.off, ptr(dz), x.n, x.h, x.w, x.c, cout,
+         ptr(dw), dw_cols, ws.data_ptr(), ws.numel(), stream_ptr())
+
+
+def im2col_c3(dt, x, n, h_valid, h, w, cols):
+    call("cnnitmo_im2col_c3", dt, ptr(x), n, h_valid, h, w, ptr(cols), stream_ptr())
+
+
+def tconv_fwd(dt, x: View, k, bias, out: View, flags=0, aff=None, stats=None):
+    assert x.ld == x.c and x.off == 0
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_tconv2x2_fwd", dt, x.ptr, x.n, x.h, x.w, x.c, ptr(k), ptr(bias), out.c, out.ptr,
+         out.ld, out.off, flags, ptr(sc), ptr(sh), ptr(stats), stream_ptr())
+
+
+def tconv_dgrad(dt, dout, n, h, w, cout, kT, cin, dx):
+    call("cnnitmo_tconv2x2_dgrad", dt, ptr(dout), n, h, w, cout, ptr(kT), cin, ptr(dx), stream_ptr())
+
+
+def tconv_wgrad(dt, x: View, dout, cout, dk):
+    assert x.ld == x.c and x.off == 0
+    nbytes = query("cnnitmo_tconv2x2_wgrad_workspace_bytes", dt, x.n, x.h, x.w, x.c, cout)
+    ws = workspace(nbytes, dout.device)
+    call("cnnitmo_tconv2x2_wgrad", dt, x.ptr, ptr(dout), x.n, x.h, x.w, x.c, cout, ptr(dk),
+         ws.data_ptr(), ws.numel(), stream_ptr())
+
+
+def prep_conv3x3(dt, w32, cout, cin, wf, wflip):
+    call("cnnitmo_prep_conv3x3_weights", dt, ptr(w32), cout, cin, ptr(wf), ptr(wflip), stream_ptr())
+
+
+def prep_tconv(dt, k32, cout, cin, kf, kT):
+    call("cnnitmo_prep_tconv2x2_weights", dt, ptr(k32), cout, cin, ptr(kf), ptr(kT), stream_ptr())
+
+
+def prep_c3(dt, w32, cout, wp):
+    call("cnnitmo_prep_c3_weights", dt, ptr(w32), cout, ptr(wp), stream_ptr())
+
+
+# ---------------------------------------------------------------- pooling
+def maxpool_fwd(dt, x: View, y, idx):
+    call("cnnitmo_maxpool2x2_fwd", dt, x.ptr, x.ld, x.off, x.n, x.h, x.w, x.c, ptr(y), ptr(idx),
+         stream_ptr())
+
+
+def maxpool_bwd(dt, dy, idx, dx: View):
+    call("cnnitmo_maxpool2x2_bwd", dt, ptr(dy), ptr(idx), dx.n, dx.h, dx.w, dx.c, dx.ptr, dx.ld,
+         dx.off, stream_ptr())
+
+
+# ---------------------------------------------------------------- batch norm
+def reduce_ws(rows, cols, device):
+    return workspace(query("cnnitmo_reduce_workspace_bytes", rows, cols), device)
+
+
+def bn_fwd_finalize(stats, rows, c, groups, count, gamma, beta, mmean, mvar, momentum, eps,
+                    scale, shift, smean, sinv):
+    ws = reduce_ws(rows, 2 * groups * c, stats.device)
+    call("cnnitmo_bn_fwd_finalize", ptr(stats), rows, c, groups, float(count), ptr(gamma), ptr(beta),
+         ptr(mmean), ptr(mvar), momentum, eps, ptr(scale), ptr(shift), ptr(smean), ptr(sinv),
+         ws.data_ptr(), stream_ptr())
+
+
+def bn_infer_coeffs(c, gamma, beta, mmean, mvar, eps, scale, shift):
+    call("cnnitmo_bn_infer_coeffs", c, ptr(gamma), ptr(beta), ptr(mmean), ptr(mvar), eps, ptr(scale),
+         ptr(shift), stream_ptr())
+
+
+def bn_apply(dt, r, p, c, scale, shift, y: View, flags=0, seed=0, layer=0):
+    call("cnnitmo_bn_apply", dt, ptr(r), p, c, ptr(scale), ptr(shift), y.ptr, y.ld, y.off, flags,
+         seed, layer, stream_ptr())
+
+
+def bn_bwd_rows(p, c):
+    return query("cnnitmo_bn_bwd_rows", p, c)
+
+
+def bn_bwd_reduce(dt, dy: View, r, c, mean, inv, flags, seed, layer, part):
+    call("cnnitmo_bn_bwd_reduce", dt, dy.ptr, dy.ld, dy.off, ptr(r), dy.p, c, ptr(mean), ptr(inv),
+         flags, seed, layer, ptr(part), stream_ptr())
+
+
+def bn_bwd_finalize(part, rows, c, count, gamma, mean, inv, dgamma, dbeta, coef):
+    ws = reduce_ws(rows, 2 * c, part.device)
+    call("cnnitmo_bn_bwd_finalize", ptr(part), rows, c, float(count), ptr(gamma), ptr(mean), ptr(inv),
+         ptr(dgamma), ptr(dbeta), ptr(coef), ws.data_ptr(), stream_ptr())
+
+
+def bn_bwd_apply(dt, dy: View, r, c, coef, flags, seed, layer, dz, part):
+    call("cnnitmo_bn_bwd_apply", dt, dy.ptr, dy.ld, dy.off, ptr(r), dy.p, c, ptr(coef), flags, seed,
+         layer, ptr(dz), ptr(part), stream_ptr())
+
+
+def colsum(part, rows, cols, groups, out):
+    ws = reduce_ws(rows, cols, part.device)
+    call("cnnitmo_colsum", ptr(part), rows, cols, groups, ptr(out), ws.data_ptr(), stream_ptr())
+
+
+# ---------------------------------------------------------------- head / optimizer
+def head_fwd(dt, x: View, h_valid, wt, b, yhat):
+    call("cnnitmo_head_fwd", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b), ptr(yhat),
+         stream_ptr())
+
+
+def head_fwd_bwd(dt, x: View, h_valid, wt, b, target, dx, part):
+    call("cnnitmo_head_fwd_bwd", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b),
+         ptr(target), ptr(dx), ptr(part), stream_ptr())
+
+
+def head_rows(p):
+    return query("cnnitmo_head_rows", p)
+
+
+def head_finalize(part, rows, cin, numel, loss_acc, dw, db):
+    ws = reduce_ws(rows, 5 + 3 * cin, part.device)
+    call("cnnitmo_head_finalize", ptr(part), rows, cin, float(numel), ptr(loss_acc), ptr(dw), ptr(db),
+         ws.data_ptr(), stream_ptr())
+
+
+def rmsprop(p, g, a, lr, rho, eps, grad_scale=1.0):
+    call("cnnitmo_rmsprop", ptr(p), ptr(g), ptr(a), p.numel(), lr, rho, eps, grad_scale, stream_ptr())

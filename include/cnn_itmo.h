@@ -1,0 +1,216 @@
+/*
+ * cnn_itmo.h -- C ABI of libcnnitmo.so, the MI355X (gfx950) kernels behind the
+ * CNN-ITMO U-Net hot path.
+ *
+ * The reference (LynxHack/CNN-ITMO) reaches its arithmetic through the Keras
+ * functional Layer API (Conv2D, Conv2DTranspose, MaxPooling2D,
+ * BatchNormalization, Activation, Dropout, concatenate) at
+ * /root/reference/model.py:195-281; TensorFlow/cuDNN execute it.  Each entry
+ * point below replaces one of those layer calls (forward or its gradient); the
+ * Python host side (cnn_itmo_amd/) mirrors the Keras API and calls these.
+ *
+ * Conventions
+ *   - Every function is stateless, never allocates, and enqueues work on the
+ *     given HIP stream (hipStream_t passed as void*).  Scratch memory is
+ *     caller-owned; size it with the *_workspace_bytes / *_rows queries.
+ *   - Return value: 0 = ok, negative = error (CNNITMO_E*);
+ *     cnnitmo_last_error() returns a thread-local message.
+ *   - dtype: CNNITMO_F32 (fp32 storage) or CNNITMO_BF16 (bf16 storage).
+ *     Accumulation is always fp32 (MFMA f32 accumulators).
+ *   - Activations are NHWC.  A "view" of an activation is (ptr, ld, off):
+ *     element (p, c) of a P-pixel, C-channel view lives at ptr[p*ld + off + c].
+ *     This is how channel concatenation (model.py:246,251,256,261) is zero-copy:
+ *     producers write channel slices of one buffer.
+ *   - Weight layouts: Conv2D OHWI [Cout][kh][kw][Cin]; Conv2DTranspose
+ *     [2][2][Cout][Cin] (Keras' own kernel layout, layers.txt:78).  Master
+ *     weights are fp32; cnnitmo_prep_* produce the dtype copies kernels read.
+ *   - Per-channel fp32 vectors (bias, BN gamma/beta/stats) are always fp32.
+ */
+#ifndef CNN_ITMO_H_
+#define CNN_ITMO_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CNNITMO_F32 0
+#define CNNITMO_BF16 1
+
+#define CNNITMO_OK 0
+#define CNNITMO_EINVAL (-1)
+#define CNNITMO_EUNSUPPORTED (-2)
+#define CNNITMO_ELAUNCH (-3)
+
+/* Epilogue flags for the forward convolutions. */
+#define CNNITMO_RELU 1   /* Activation('relu') after the conv (model.py:196,200) */
+#define CNNITMO_STATS 2  /* write per-tile BN partial sums (sum, sum of squares) */
+#define CNNITMO_AFFINE 4 /* y = v*scale[c] + shift[c] after ReLU (inference BN) */
+
+/* Flags for BN apply / backward. */
+#define CNNITMO_DROPOUT 1 /* Dropout(0.5), model.py:226,239 (train only) */
+#define CNNITMO_NO_BN 2   /* bwd: plain ReLU gradient, no BN (config-1 net)  */
+
+int cnnitmo_version(void);
+const char* cnnitmo_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Conv2D(f, 3, padding='same') -- replaces Conv2D at model.py:196 (via ConvBN).
+ * x view: [n, h, w, cin] (ld, off); wt: [cout][3][3][cin] in dtype.
+ * out view: [n, h, w, cout] (ld, off).  flags: CNNITMO_RELU|STATS|AFFINE.
+ * stat_part (STATS): [rows][2][cout] fp32, rows = cnnitmo_fwd_stat_rows(...).
+ * aff_scale/aff_shift (AFFINE): [cout] fp32.
+ * Requires cin % 32 == 0 (bf16) or % 16 == 0 (f32), cout % 32 == 0.
+ */
+int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w,
+                        int cin, const void* wt, const float* bias, int cout, void* out,
+                        int out_ld, int out_off, int flags, const float* aff_scale,
+                        const float* aff_shift, float* stat_part, void* stream);
+
+/* Rows of the BN partial-sum buffer written by a forward conv over m output
+ * pixels with ncols GEMM columns (cout for conv3x3, 4*cout for tconv2x2). */
+int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols);
+
+/* Input-gradient of conv3x3 (TF Conv2DBackpropInput).  dz: [n,h,w,cout]
+ * contiguous; wt_flip: [cin][3][3][cout] = W[co][2-r][2-s][ci] (from
+ * cnnitmo_prep_conv3x3_weights).  dx view [n,h,w,cin] (ld, off) is OVERWRITTEN. */
+int cnnitmo_conv3x3_dgrad(int dtype, const void* dz, int n, int h, int w, int cout,
+                          const void* wt_flip, int cin, void* dx, int dx_ld, int dx_off,
+                          void* stream);
+
+/* Weight-gradient of conv3x3 (TF Conv2DBackpropFilter).  x view [n,h,w,cin];
+ * dz [n,h,w,cout] contiguous; dw: [cout][3][3][cin] fp32, OVERWRITTEN.
+ * ntaps = 9 for the 3x3 conv, 1 for a 1x1 / pre-packed (im2col) input. */
+size_t cnnitmo_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin, int cout,
+                                     int ntaps);
+int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
+                       const void* dz, int n, int h, int w, int cin, int cout, float* dw,
+                       int dw_cols, void* workspace, size_t ws_bytes, void* stream);
+
+/* First layer (Cin=3): pack x [n,h_valid,w,3] fp32 into [n,h,w,32] dtype
+ * columns k=(r*3+s)*3+c (k<27, zero pad; rows >= h_valid are zero), so that
+ * conv2d_1 runs as a 1-tap GEMM with K=32.  Fuses the /255 input's cast and
+ * the pad-to-multiple-of-16 of predict.py:59 / SURVEY 8a. */
+int cnnitmo_im2col_c3(int dtype, const float* x, int n, int h_valid, int h, int w, void* cols,
+                      void* stream);
+/* 1-tap GEMM forward over packed columns: out = cols[m][k] * wt[cout][k]. */
+int cnnitmo_conv1tap_fwd(int dtype, const void* cols, int k, long m, const void* wt,
+                         const float* bias, int cout, void* out, int out_ld, int out_off,
+                         int flags, const float* aff_scale, const float* aff_shift,
+                         float* stat_part, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Conv2DTranspose(f, 2, strides=2, 'valid') -- replaces model.py:200
+ * (ConvBNTranspose).  x [n,h,w,cin] contiguous; k: [2][2][cout][cin] dtype;
+ * out view [n,2h,2w,cout] (ld, off); flags/stat_part as conv3x3 (stat_part
+ * columns are [4*cout] = (tap, channel)).
+ */
+int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int w, int cin, const void* k,
+                         const float* bias, int cout, void* out, int out_ld, int out_off,
+                         int flags, const float* aff_scale, const float* aff_shift,
+                         float* stat_part, void* stream);
+/* dx [n,h,w,cin] (contiguous, OVERWRITTEN) from dout [n,2h,2w,cout] and
+ * kT: [cin][2][2][cout] (from cnnitmo_prep_tconv2x2_weights). */
+int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h, int w, int cout,
+                           const void* kT, int cin, void* dx, void* stream);
+/* dk [2][2][cout][cin] fp32 (OVERWRITTEN) from x [n,h,w,cin], dout [n,2h,2w,cout]. */
+int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h, int w,
+                           int cin, int cout, float* dk, void* workspace, size_t ws_bytes,
+                           void* stream);
+size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin, int cout);
+
+/* Weight preparation (after every optimizer step): fp32 master -> dtype copies.
+ * conv3x3: w [cout][3][3][cin] -> w_fwd (same layout), w_flip [cin][3][3][cout].
+ * w_flip may be NULL (first layer).  tconv: k [2][2][cout][cin] -> k_fwd (same),
+ * kT [cin][2][2][cout].  pack_c3: w [32][3][3][3] -> [32][32] zero-padded. */
+int cnnitmo_prep_conv3x3_weights(int dtype, const float* w, int cout, int cin, void* w_fwd,
+                                 void* w_flip, void* stream);
+int cnnitmo_prep_tconv2x2_weights(int dtype, const float* k, int cout, int cin, void* k_fwd,
+                                  void* kT, void* stream);
+int cnnitmo_prep_c3_weights(int dtype, const float* w, int cout, void* w_packed, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * MaxPooling2D(pool_size=(2,2), strides=2) -- model.py:210,215,220,227.
+ * fwd: x view [n,h,w,c] -> y [n,h/2,w/2,c] contiguous + argmax idx uint8 (0..3,
+ * first maximum in row-major window order).
+ * bwd: dx view [n,h,w,c] += scatter of dy to the argmax (other entries untouched).
+ */
+int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w,
+                           int c, void* y, uint8_t* idx, void* stream);
+int cnnitmo_maxpool2x2_bwd(int dtype, const void* dy, const uint8_t* idx, int n, int h, int w,
+                           int c, void* dx, int dx_ld, int dx_off, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * BatchNormalization() (axis=-1, eps 1e-3, momentum 0.99) -- model.py:196,200.
+ * Training forward: the conv epilogue writes r = relu(conv) and partial sums;
+ * cnnitmo_bn_fwd_finalize reduces them (fp64) to batch mean / biased variance,
+ * produces scale = gamma*invstd, shift = beta - mean*scale, saves mean/invstd for
+ * backward and updates the moving statistics (Keras-2.2: var *= n/(n-(1+eps))).
+ * groups: the stat_part columns are [groups][c] (4 for a tconv, else 1).
+ * workspace: cnnitmo_reduce_workspace_bytes(rows, groups*c*2).
+ */
+size_t cnnitmo_reduce_workspace_bytes(long rows, int cols);
+int cnnitmo_bn_fwd_finalize(const float* stat_part, long rows, int c, int groups, double count,
+                            const float* gamma, const float* beta, float* moving_mean,
+                            float* moving_var, float momentum, float eps, float* scale,
+                            float* shift, float* save_mean, float* save_invstd,
+                            void* workspace, void* stream);
+/* Inference-mode coefficients from the moving statistics. */
+int cnnitmo_bn_infer_coeffs(int c, const float* gamma, const float* beta, const float* mmean,
+                            const float* mvar, float eps, float* scale, float* shift,
+                            void* stream);
+/* y view = r*scale + shift (optionally Dropout(0.5): element (p,c) kept iff the
+ * counter hash of (seed, layer, p*c_total + c) says so, kept values x2). */
+int cnnitmo_bn_apply(int dtype, const void* r, long p, int c, const float* scale,
+                     const float* shift, void* y, int y_ld, int y_off, int flags,
+                     uint64_t drop_seed, int drop_layer, void* stream);
+/* Backward.  dy view (ld, off) is the gradient w.r.t. the BN (or dropout)
+ * output; r is the saved post-ReLU tensor [p][c].
+ * Step 1 (reduce+finalize): dgamma, dbeta (written, fp32) and the three dz
+ * coefficients.  Step 2 (apply): dz = [r>0]*(a*dy' - b*r + e) -> dz [p][c] and
+ * the bias gradient db (written).  With CNNITMO_NO_BN: dz = [r>0]*dy. */
+int cnnitmo_bn_bwd_rows(long p, int c);
+int cnnitmo_bn_bwd_reduce(int dtype, const void* dy, int dy_ld, int dy_off, const void* r,
+                          long p, int c, const float* mean, const float* invstd, int flags,
+                          uint64_t drop_seed, int drop_layer, float* part, void* stream);
+int cnnitmo_bn_bwd_finalize(const float* part, long rows, int c, double count,
+                            const float* gamma, const float* mean, const float* invstd,
+                            float* dgamma, float* dbeta, float* coef, void* workspace,
+                            void* stream);
+int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off, const void* r, long p,
+                         int c, const float* coef, int flags, uint64_t drop_seed, int drop_layer,
+                         void* dz, float* part, void* stream);
+/* Column sums of partial rows -> out[groups-folded c] (fp32, written). */
+int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* out,
+                   void* workspace, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Head: Conv2D(3, 1, activation='sigmoid') + MSE loss + 'accuracy'
+ * (model.py:276,281).  x [p][64-ish cin] dtype; w [3][cin] fp32, b [3].
+ * fwd: yhat [n,h,w,3] fp32 for rows < h_valid (predict.py:62).
+ * fwd_bwd: target [n,h_valid,w,3] fp32; writes dx [p][cin] dtype
+ * (= dz * W), and partials (loss sum, correct count, dW, db) into part;
+ * cnnitmo_head_finalize reduces them into loss, acc, dw, db. */
+int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
+                     const float* wt, const float* b, float* yhat, void* stream);
+int cnnitmo_head_rows(long p);
+int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
+                         const float* wt, const float* b, const float* target, void* dx,
+                         float* part, void* stream);
+int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel, float* loss_acc,
+                          float* dw, float* db, void* workspace, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * RMSprop (keras.optimizers.RMSprop defaults via compile('rmsprop'), model.py:281):
+ *   a <- rho*a + (1-rho)*g'^2 ; p <- p - lr*g'/(sqrt(a)+eps),  g' = g*grad_scale
+ * over one flat fp32 buffer holding every trainable tensor (multi-tensor apply).
+ */
+int cnnitmo_rmsprop(float* p, const float* g, float* a, long n, float lr, float rho, float eps,
+                    float grad_scale, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CNN_ITMO_H_ */

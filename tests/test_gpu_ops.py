@@ -1,0 +1,304 @@
+"""Per-kernel parity: every C-ABI entry point vs the numpy oracle (fp64) on the
+same seeded inputs.  fp32 path: max-abs <= 1e-4 relative to the output scale
+(MFMA f32 is an exact fp32 fma chain).  bf16 path: inputs are rounded to bf16
+first and the oracle sees the same rounded values; tolerance 1.5e-2 of scale
+(bf16 output rounding is 2^-8)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import unet_ref as R  # noqa: E402
+
+DT = {"f32": 0, "bf16": 1}
+TDT = {"f32": torch.float32, "bf16": torch.bfloat16}
+TOL = {"f32": 1e-4, "bf16": 1.5e-2}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_itmo_amd import _lib as L
+    L.load()
+
+
+def dev(a, dt):
+    return torch.tensor(np.ascontiguousarray(a), dtype=torch.float32).to(TDT[dt]).cuda()
+
+
+def rnd(a, dt):
+    """Round host array through the device dtype (what the kernel actually sees)."""
+    return torch.tensor(np.ascontiguousarray(a), dtype=torch.float32).to(TDT[dt]).double().numpy()
+
+
+def host(t):
+    return t.float().cpu().numpy().astype(np.float64)
+
+
+def close(got, want, dt, what=""):
+    scale = max(1.0, float(np.abs(want).max()))
+    err = float(np.abs(got - want).max())
+    assert err <= TOL[dt] * scale, f"{what}: max-abs err {err:.3e} > {TOL[dt] * scale:.3e}"
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 8, 12), (64, 128, 5, 7), (96, 64, 6, 10), (32, 256, 4, 4)])
+def test_conv3x3_fwd_dgrad_wgrad(dt, cin, cout, H, W):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin + cout)
+    N = 2
+    # input lives in a wider buffer (zero-copy concat view): ld = cin + 32, off = 32
+    ld, off = cin + 32, 32
+    xb = rng.standard_normal((N, H, W, ld)).astype(np.float32)
+    w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    x = rnd(xb, dt)[..., off:]
+    wr = rnd(w, dt)
+    z = R.conv2d_same(x, wr, b)
+    r_ref = np.maximum(z, 0)
+    xbuf = dev(xb, dt).reshape(-1)
+    xv = ops.View(xbuf, N, H, W, cin, ld, off)
+    d = DT[dt]
+    wf = torch.empty(w.size, dtype=TDT[dt], device="cuda")
+    wflip = torch.empty(w.size, dtype=TDT[dt], device="cuda")
+    ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cin, wf, wflip)
+    out = ops.new_view(N, H, W, cout, TDT[dt])
+    rows = ops.fwd_stat_rows(d, N * H * W, cout)
+    stats = torch.zeros(rows, 2, cout, device="cuda")
+    ops.conv3x3_fwd(d, xv, wf, torch.tensor(b).cuda(), out, flags=1 | 2, stats=stats)
+    torch.cuda.synchronize()
+    close(host(out.buf).reshape(N, H, W, cout), r_ref, dt, "fwd")
+    s = stats.sum(0).double().cpu().numpy()
+    close(s[0] / r_ref.size * cout, r_ref.reshape(-1, cout).mean(0), dt, "stat sum")
+    # dgrad into a view of a wider buffer
+    dz = rng.standard_normal((N, H, W, cout)).astype(np.float32)
+    dzr = rnd(dz, dt)
+    dx_ref, dw_ref, db_ref = R.conv2d_same_bwd(x, wr, dzr)
+    dxb = torch.zeros(N * H * W * ld, dtype=TDT[dt], device="cuda")
+    ops.conv3x3_dgrad(d, dev(dz, dt), N, H, W, cout, wflip, cin, ops.View(dxb, N, H, W, cin, ld, off))
+    torch.cuda.synchronize()
+    close(host(dxb).reshape(N, H, W, ld)[..., off:], dx_ref, dt, "dgrad")
+    assert float(host(dxb).reshape(N, H, W, ld)[..., :off].max()) == 0.0  # other slice untouched
+    dw = torch.empty(cout, 3, 3, cin, device="cuda")
+    ops.conv_wgrad(d, 9, xv, dev(dz, dt), cout, dw)
+    torch.cuda.synchronize()
+    close(host(dw), dw_ref, dt, "wgrad")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_conv_affine_inference_epilogue(dt):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(3)
+    N, H, W, cin, cout = 1, 6, 9, 32, 64
+    x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
+    w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    sc = rng.uniform(0.5, 2, cout).astype(np.float32)
+    sh = rng.standard_normal(cout).astype(np.float32)
+    d = DT[dt]
+    wf = torch.empty(w.size, dtype=TDT[dt], device="cuda")
+    ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cin, wf, None)
+    out = ops.new_view(N, H, W, cout, TDT[dt])
+    ops.conv3x3_fwd(d, ops.View(dev(x, dt).reshape(-1), N, H, W, cin, cin), wf, torch.tensor(b).cuda(), out,
+                    flags=1 | 4, aff=(torch.tensor(sc).cuda(), torch.tensor(sh).cuda()))
+    ref = np.maximum(R.conv2d_same(rnd(x, dt), rnd(w, dt), b), 0) * sc + sh
+    torch.cuda.synchronize()
+    close(host(out.buf).reshape(ref.shape), ref, dt, "affine")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("cin,cout,H,W", [(64, 32, 3, 5), (128, 64, 4, 4), (512, 256, 2, 3)])
+def test_tconv(dt, cin, cout, H, W):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin)
+    N = 2
+    x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
+    k = (rng.standard_normal((2, 2, cout, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    d = DT[dt]
+    xr, kr = rnd(x, dt), rnd(k, dt)
+    ref = np.maximum(R.tconv2x2s2(xr, kr, b), 0)
+    kf = torch.empty(k.size, dtype=TDT[dt], device="cuda")
+    kT = torch.empty(k.size, dtype=TDT[dt], device="cuda")
+    ops.prep_tconv(d, torch.tensor(k).cuda(), cout, cin, kf, kT)
+    # output into a concat slice: ld = cout + 64, off = 64
+    ld = cout + 64
+    ob = torch.zeros(N * 2 * H * 2 * W * ld, dtype=TDT[dt], device="cuda")
+    rows = ops.fwd_stat_rows(d, N * H * W, 4 * cout)
+    stats = torch.zeros(rows, 2, 4 * cout, device="cuda")
+    xv = ops.View(dev(x, dt).reshape(-1), N, H, W, cin, cin)
+    ops.tconv_fwd(d, xv, kf, torch.tensor(b).cuda(), ops.View(ob, N, 2 * H, 2 * W, cout, ld, 64),
+                  flags=1 | 2, stats=stats)
+    torch.cuda.synchronize()
+    got = host(ob).reshape(N, 2 * H, 2 * W, ld)
+    close(got[..., 64:], ref, dt, "tconv fwd")
+    s = stats.sum(0).double().cpu().numpy()[0].reshape(4, cout).sum(0)
+    close(s / (ref.size / cout), ref.reshape(-1, cout).mean(0), dt, "tconv stats")
+    dout = rng.standard_normal((N, 2 * H, 2 * W, cout)).astype(np.float32)
+    dx_ref, dk_ref, _ = R.tconv2x2s2_bwd(xr, kr, rnd(dout, dt))
+    dx = torch.empty(N * H * W * cin, dtype=TDT[dt], device="cuda")
+    ops.tconv_dgrad(d, dev(dout, dt), N, H, W, cout, kT, cin, dx)
+    dk = torch.empty(2, 2, cout, cin, device="cuda")
+    ops.tconv_wgrad(d, xv, dev(dout, dt), cout, dk)
+    torch.cuda.synchronize()
+    close(host(dx).reshape(dx_ref.shape), dx_ref, dt, "tconv dgrad")
+    close(host(dk), dk_ref, dt, "tconv wgrad")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_first_layer_im2col(dt):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(9)
+    N, Hv, H, W = 2, 13, 16, 10
+    x = rng.uniform(size=(N, Hv, W, 3)).astype(np.float32)
+    w = (rng.standard_normal((32, 3, 3, 3)) * 0.3).astype(np.float32)
+    b = rng.standard_normal(32).astype(np.float32)
+    d = DT[dt]
+    cols = torch.empty(N * H * W * 32, dtype=TDT[dt], device="cuda")
+    ops.im2col_c3(d, torch.tensor(x).cuda(), N, Hv, H, W, cols)
+    wp = torch.empty(32 * 32, dtype=TDT[dt], device="cuda")
+    ops.prep_c3(d, torch.tensor(w).cuda(), 32, wp)
+    out = ops.new_view(N, H, W, 32, TDT[dt])
+    ops.conv1tap_fwd(d, cols, 32, N * H * W, wp, torch.tensor(b).cuda(), out, flags=1)
+    xp = np.zeros((N, H, W, 3))
+    xp[:, :Hv] = rnd(x, dt)
+    ref = np.maximum(R.conv2d_same(xp, rnd(w, dt), b), 0)
+    torch.cuda.synchronize()
+    close(host(out.buf).reshape(ref.shape), ref, dt, "first layer")
+    dz = rng.standard_normal((N, H, W, 32)).astype(np.float32)
+    _, dw_ref, _ = R.conv2d_same_bwd(xp, rnd(w, dt), rnd(dz, dt), need_dx=False)
+    dw = torch.empty(32, 27, device="cuda")
+    ops.conv_wgrad(d, 1, ops.View(cols, N, H, W, 32, 32), dev(dz, dt), 32, dw, dw_cols=27)
+    torch.cuda.synchronize()
+    close(host(dw).reshape(dw_ref.shape), dw_ref, dt, "first layer wgrad")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_maxpool_ties(dt):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(4)
+    N, H, W, C, ld, off = 2, 6, 8, 32, 96, 64
+    xb = rng.integers(-2, 3, size=(N, H, W, ld)).astype(np.float32)  # many ties
+    d = DT[dt]
+    xv = ops.View(dev(xb, dt).reshape(-1), N, H, W, C, ld, off)
+    y = torch.empty(N * H // 2 * W // 2 * C, dtype=TDT[dt], device="cuda")
+    idx = torch.empty(N * H // 2 * W // 2 * C, dtype=torch.uint8, device="cuda")
+    ops.maxpool_fwd(d, xv, y, idx)
+    yr, ir = R.maxpool2x2(xb[..., off:].astype(np.float64))
+    dy = rng.standard_normal(yr.shape).astype(np.float32)
+    base = rng.standard_normal((N, H, W, ld)).astype(np.float32)
+    dxb = dev(base, dt).reshape(-1)
+    ops.maxpool_bwd(d, dev(dy, dt), idx, ops.View(dxb, N, H, W, C, ld, off))
+    torch.cuda.synchronize()
+    assert np.array_equal(host(y).reshape(yr.shape), yr)
+    assert np.array_equal(idx.cpu().numpy().reshape(ir.shape), ir)
+    want = rnd(base, dt)
+    want[..., off:] += R.maxpool2x2_bwd(rnd(dy, dt), ir, (N, H, W, C))
+    close(host(dxb).reshape(want.shape), want, dt, "pool bwd")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("drop", [False, True])
+def test_bn_train_fwd_bwd(dt, drop):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(5)
+    N, H, W, C = 2, 5, 7, 64
+    P = N * H * W
+    r = np.maximum(rng.standard_normal((N, H, W, C)), 0).astype(np.float32)
+    g = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    be = rng.standard_normal(C).astype(np.float32)
+    rr = rnd(r, dt)
+    d = DT[dt]
+    rt = dev(r, dt)
+    # stats as the conv epilogue would produce them (one row)
+    stats = torch.tensor(np.stack([rr.reshape(-1, C).sum(0), (rr.reshape(-1, C) ** 2).sum(0)])[None],
+                         dtype=torch.float32).cuda()
+    cu = lambda a: torch.tensor(a, dtype=torch.float32).cuda()
+    mm, mv = cu(np.zeros(C)), cu(np.ones(C))
+    sc, sh, sm, si = (torch.empty(C, device="cuda") for _ in range(4))
+    ops.bn_fwd_finalize(stats, 1, C, 1, P, cu(g), cu(be), mm, mv, 0.99, 1e-3, sc, sh, sm, si)
+    ld, off = C + 32, 32
+    yb = torch.zeros(P * ld, dtype=TDT[dt], device="cuda")
+    seed, layer = 123, 1
+    ops.bn_apply(d, rt, P, C, sc, sh, ops.View(yb, N, H, W, C, ld, off), flags=1 if drop else 0,
+                 seed=seed, layer=layer)
+    y_ref, m_ref, v_ref = R.bn_train_fwd(rr, g, be)
+    if drop:
+        y_ref, keep = R.dropout_fwd(y_ref, seed, layer)
+    mm_ref, mv_ref = R.bn_moving_update(np.zeros(C), np.ones(C), m_ref, v_ref, P)
+    torch.cuda.synchronize()
+    close(host(yb).reshape(N, H, W, ld)[..., off:], y_ref, dt, "bn apply")
+    np.testing.assert_allclose(mm.cpu().numpy(), mm_ref, atol=1e-5)
+    np.testing.assert_allclose(mv.cpu().numpy(), mv_ref, atol=1e-5)
+    # backward from a dy view
+    dyb = rng.standard_normal((N, H, W, ld)).astype(np.float32)
+    dy = rnd(dyb, dt)[..., off:]
+    dyv = ops.View(dev(dyb, dt).reshape(-1), N, H, W, C, ld, off)
+    flags = 1 if drop else 0
+    rows = ops.bn_bwd_rows(P, C)
+    part = torch.empty(rows, 2, C, device="cuda")
+    ops.bn_bwd_reduce(d, dyv, rt, C, sm, si, flags, seed, layer, part)
+    dgam, dbet, coef = torch.empty(C, device="cuda"), torch.empty(C, device="cuda"), torch.empty(3, C, device="cuda")
+    ops.bn_bwd_finalize(part, rows, C, P, cu(g), sm, si, dgam, dbet, coef)
+    dz = torch.empty(P * C, dtype=TDT[dt], device="cuda")
+    part2 = torch.empty(rows, C, device="cuda")
+    ops.bn_bwd_apply(d, dyv, rt, C, coef, flags, seed, layer, dz, part2)
+    db = torch.empty(C, device="cuda")
+    ops.colsum(part2, rows, C, 1, db)
+    dyd = dy * keep * 2.0 if drop else dy
+    dr, dg_ref, dbeta_ref = R.bn_train_bwd(dyd, rr, g, m_ref, v_ref)
+    dz_ref = dr * (rr > 0)
+    torch.cuda.synchronize()
+    close(host(dgam), dg_ref, dt, "dgamma")
+    close(host(dbet), dbeta_ref, dt, "dbeta")
+    close(host(dz).reshape(dz_ref.shape), dz_ref, dt, "dz")
+    close(host(db), dz_ref.reshape(-1, C).sum(0), dt, "db")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_head(dt):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(6)
+    N, Hv, H, W, C = 2, 7, 8, 16, 64
+    x = rng.standard_normal((N, H, W, C)).astype(np.float32)
+    w = (rng.standard_normal((3, C)) * 0.2).astype(np.float32)
+    b = rng.standard_normal(3).astype(np.float32)
+    t = rng.uniform(size=(N, Hv, W, 3)).astype(np.float32)
+    d = DT[dt]
+    xv = ops.View(dev(x, dt).reshape(-1), N, H, W, C, C)
+    cu = lambda a: torch.tensor(a, dtype=torch.float32).cuda()
+    yh = torch.empty(N, Hv, W, 3, device="cuda")
+    ops.head_fwd(d, xv, Hv, cu(w), cu(b), yh)
+    xr = rnd(x, dt)[:, :Hv]
+    yref = R.sigmoid(xr @ w.T.astype(np.float64) + b)
+    rows = ops.head_rows(N * H * W)
+    part = torch.empty(rows, 5 + 3 * C, device="cuda")
+    dx = torch.empty(N * H * W * C, dtype=TDT[dt], device="cuda")
+    ops.head_fwd_bwd(d, xv, Hv, cu(w), cu(b), cu(t), dx, part)
+    la, dw, db = torch.empty(2, device="cuda"), torch.empty(3, C, device="cuda"), torch.empty(3, device="cuda")
+    ops.head_finalize(part, rows, C, N * Hv * W * 3, la, dw, db)
+    dz = R.mse_grad_z(yref, t)
+    dx_ref = np.zeros((N, H, W, C))
+    dx_ref[:, :Hv] = dz @ w.astype(np.float64)
+    torch.cuda.synchronize()
+    close(yh.cpu().numpy(), yref, "f32", "yhat")
+    assert abs(la[0].item() - R.mse(yref, t)) < 1e-5
+    assert abs(la[1].item() - R.categorical_accuracy(t, yref)) < 1e-6
+    close(host(dw), dz.reshape(-1, 3).T @ xr.reshape(-1, C), "f32", "head dw")
+    close(host(db), dz.reshape(-1, 3).sum(0), "f32", "head db")
+    close(host(dx).reshape(dx_ref.shape) * 1e3, dx_ref * 1e3, dt, "head dx")
+
+
+def test_rmsprop():
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(7)
+    n = 1003
+    p, g, a = rng.standard_normal(n), rng.standard_normal(n), rng.uniform(size=n)
+    pt, gt, at = (torch.tensor(v, dtype=torch.float32).cuda() for v in (p, g, a))
+    ops.rmsprop(pt, gt, at, 1e-3, 0.9, 1e-7, grad_scale=0.5)
+    pr, ar = R.rmsprop(p, g * 0.5, a)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(pt.cpu().numpy(), pr, atol=1e-6)
+    np.testing.assert_allclose(at.cpu().numpy(), ar, atol=1e-6)
