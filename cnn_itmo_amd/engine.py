@@ -1,0 +1,555 @@
+"""Graph compiler + executor: Keras layer graph -> fused HIP-kernel stages.
+
+Fusion rules (what the reference's graph, /root/reference/model.py:195-278,
+needs; anything else raises NotImplementedError at compile time):
+
+  Conv2D(3,'same') [+Activation('relu') | activation='relu'] [+BatchNormalization] [+Dropout]
+      -> BlockStage 'c3'   (conv epilogue: bias+ReLU+BN partial sums; BN-apply(+dropout)
+                            writes straight into its consumer's buffer / concat slice)
+  first Conv2D(3,'same') on the 3-channel Input -> BlockStage 'c3in' (im2col-packed 1-tap GEMM)
+  Conv2DTranspose(2, strides=2) + ReLU + BN      -> BlockStage 't2' (pixel-scatter epilogue)
+  MaxPooling2D(2)                                -> PoolStage
+  concatenate([...])                             -> ConcatStage (zero-copy: inputs are placed
+                                                    as channel slices of one buffer)
+  final Conv2D(3, 1, activation='sigmoid')       -> HeadStage (sigmoid + MSE + accuracy + grads)
+
+Training BN uses per-replica batch statistics (Keras semantics per process).
+Every parameter lives in one flat fp32 buffer laid out in REVERSE stage order,
+so backward produces gradients front-to-back -- the order the data-parallel
+bucketer (dist.py) all-reduces them in.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+from . import _lib as L
+from .layers import (Activation, BatchNormalization, Concatenate, Conv2D, Conv2DTranspose, Dropout,
+                     InputLayer, MaxPooling2D)
+
+ALIGN = 16  # floats
+
+
+class Value:
+    """A materialised activation [n, h, w, c] (optionally a channel slice of a concat)."""
+
+    def __init__(self, name, shape):
+        self.name = name
+        self.h, self.w, self.c = shape
+        self.place = None  # (concat Value, channel offset)
+        self.members = []  # for concat values: placed member Values
+        self.buf = None
+        self.gbuf = None
+        self.ginit = False
+        self.needs_grad = True
+
+    def owner(self):
+        return self.place[0] if self.place else self
+
+    def view(self, n):
+        if self.place:
+            cv, off = self.place
+            return ops.View(cv.buf, n, self.h, self.w, self.c, cv.c, off)
+        return ops.View(self.buf, n, self.h, self.w, self.c, self.c, 0)
+
+    def gview(self, n):
+        if self.place:
+            cv, off = self.place
+            return ops.View(cv.gbuf, n, self.h, self.w, self.c, cv.c, off)
+        return ops.View(self.gbuf, n, self.h, self.w, self.c, self.c, 0)
+
+    def ensure(self, n, dtype, device):
+        o = self.owner()
+        if o.buf is None:
+            o.buf = torch.empty(n * o.h * o.w * o.c, dtype=dtype, device=device)
+
+    def ensure_grad(self, n, dtype, device, zero=False):
+        o = self.owner()
+        if o.gbuf is None:
+            o.gbuf = (torch.zeros if zero else torch.empty)(n * o.h * o.w * o.c, dtype=dtype, device=device)
+            if zero:
+                o.mark_grad()
+
+    def mark_grad(self):
+        self.ginit = True
+        for m in self.members:
+            m.ginit = True
+
+    def release(self):
+        self.buf = None
+        self.gbuf = None
+        self.ginit = False
+
+
+class Stage:
+    params = ()  # [(key, shape)] trainable, in flat-buffer order
+    buffers = ()  # [(key, shape)] non-trainable
+
+    def bind(self, eng):
+        self.eng = eng
+
+
+class BlockStage(Stage):
+    def __init__(self, kind, conv, relu, bn, drop, drop_id, vin, vout):
+        self.kind, self.conv, self.relu, self.bn, self.drop = kind, conv, relu, bn, drop
+        self.drop_id = drop_id
+        self.vin, self.vout = vin, vout
+        self.cin = vin.c if kind != "c3in" else 3
+        self.cout = conv.filters
+        self.name = conv.name
+        k = conv.name
+        if kind == "t2":
+            kshape = (2, 2, self.cout, self.cin)
+        else:
+            kshape = (self.cout, 3, 3, self.cin)
+        self.params = [(k + "/kernel", kshape), (k + "/bias", (self.cout,))]
+        self.buffers = []
+        if bn is not None:
+            b = bn.name
+            self.params += [(b + "/gamma", (self.cout,)), (b + "/beta", (self.cout,))]
+            self.buffers = [(b + "/moving_mean", (self.cout,)), (b + "/moving_variance", (self.cout,))]
+
+    def bind(self, eng):
+        super().bind(eng)
+        T = eng.tdtype
+        cout, cin = self.cout, self.cin
+        dev = eng.device
+        if self.kind == "c3":
+            self.w_fwd = torch.empty(cout * 9 * cin, dtype=T, device=dev)
+            self.w_bwd = torch.empty(cout * 9 * cin, dtype=T, device=dev)
+        elif self.kind == "c3in":
+            self.w_fwd = torch.empty(cout * 32, dtype=T, device=dev)
+            self.w_bwd = None
+        else:
+            self.w_fwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
+            self.w_bwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
+
+    def prep(self):
+        e = self.eng
+        w = e.p(self.conv.name + "/kernel")
+        if self.kind == "c3":
+            ops.prep_conv3x3(e.dt, w, self.cout, self.cin, self.w_fwd, self.w_bwd)
+        elif self.kind == "c3in":
+            ops.prep_c3(e.dt, w, self.cout, self.w_fwd)
+        else:
+            ops.prep_tconv(e.dt, w, self.cout, self.cin, self.w_fwd, self.w_bwd)
+
+    def _conv(self, n, out_view, flags, aff=None, stats=None):
+        e = self.eng
+        bias = e.p(self.conv.name + "/bias")
+        if self.kind == "c3":
+            ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
+        elif self.kind == "c3in":
+            ops.conv1tap_fwd(e.dt, self.cols, 32, n * self.vout.h * self.vout.w, self.w_fwd, bias,
+                             out_view, flags, aff, stats)
+        else:
+            ops.tconv_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
+
+    def _gemm_rows(self, n):
+        if self.kind == "t2":
+            return n * self.vin.h * self.vin.w, 4 * self.cout
+        return n * self.vout.h * self.vout.w, self.cout
+
+    def forward(self, n, training):
+        e = self.eng
+        cout = self.cout
+        P = n * self.vout.h * self.vout.w
+        if self.kind == "c3in":
+            self.cols = torch.empty(P * 32, dtype=e.tdtype, device=e.device)
+            ops.im2col_c3(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.cols)
+        self.vout.ensure(n, e.tdtype, e.device)
+        out = self.vout.view(n)
+        if self.bn is None:
+            if self.vout.place:
+                raise NotImplementedError("a ReLU-only conv whose output feeds a concatenate")
+            self._conv(n, out, L.RELU if self.relu else 0)
+            self.r = self.vout.buf
+            return
+        bn = self.bn
+        g, b = e.p(bn.name + "/gamma"), e.p(bn.name + "/beta")
+        mm, mv = e.b(bn.name + "/moving_mean"), e.b(bn.name + "/moving_variance")
+        if not training:
+            sc = torch.empty(cout, device=e.device)
+            sh = torch.empty(cout, device=e.device)
+            ops.bn_infer_coeffs(cout, g, b, mm, mv, bn.epsilon, sc, sh)
+            self._conv(n, out, (L.RELU if self.relu else 0) | L.AFFINE, aff=(sc, sh))
+            return
+        m, ncols = self._gemm_rows(n)
+        rows = ops.fwd_stat_rows(e.dt, m, ncols)
+        stats = torch.empty(rows * 2 * ncols, device=e.device)
+        r = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
+        self._conv(n, ops.View(r, n, self.vout.h, self.vout.w, cout, cout, 0),
+                   (L.RELU if self.relu else 0) | L.STATS, stats=stats)
+        self.scale = torch.empty(cout, device=e.device)
+        self.shift = torch.empty(cout, device=e.device)
+        self.smean = torch.empty(cout, device=e.device)
+        self.sinv = torch.empty(cout, device=e.device)
+        ops.bn_fwd_finalize(stats, rows, cout, 4 if self.kind == "t2" else 1, P, g, b,
+                            mm if e.update_moving else None, mv if e.update_moving else None,
+                            bn.momentum, bn.epsilon, self.scale, self.shift, self.smean, self.sinv)
+        flags = L.DROPOUT if self.drop is not None else 0
+        ops.bn_apply(e.dt, r, P, cout, self.scale, self.shift, out, flags, e.drop_seed, self.drop_id)
+        self.r = r
+
+    def backward(self, n):
+        e = self.eng
+        cout = self.cout
+        P = n * self.vout.h * self.vout.w
+        if not self.vout.ginit:
+            raise RuntimeError(f"{self.name}: output gradient not initialised")
+        dy = self.vout.gview(n)
+        rows = ops.bn_bwd_rows(P, cout)
+        dz = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
+        part2 = torch.empty(rows * cout, device=e.device)
+        flags = L.DROPOUT if self.drop is not None else 0
+        if self.bn is not None:
+            bn = self.bn
+            part = torch.empty(rows * 2 * cout, device=e.device)
+            ops.bn_bwd_reduce(e.dt, dy, self.r, cout, self.smean, self.sinv, flags, e.drop_seed,
+                              self.drop_id, part)
+            coef = torch.empty(3 * cout, device=e.device)
+            ops.bn_bwd_finalize(part, rows, cout, P, e.p(bn.name + "/gamma"), self.smean, self.sinv,
+                                e.g(bn.name + "/gamma"), e.g(bn.name + "/beta"), coef)
+            ops.bn_bwd_apply(e.dt, dy, self.r, cout, coef, flags, e.drop_seed, self.drop_id, dz, part2)
+        else:
+            ops.bn_bwd_apply(e.dt, dy, self.r, cout, None, flags | L.NO_BN, e.drop_seed,
+                             self.drop_id, dz, part2)
+        ops.colsum(part2, rows, cout, 1, e.g(self.conv.name + "/bias"))
+        dw = e.g(self.conv.name + "/kernel")
+        if self.kind == "c3in":
+            ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
+                           dw, dw_cols=27)
+        elif self.kind == "c3":
+            ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw)
+        else:
+            ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw)
+        if self.vin.needs_grad:
+            if self.vin.ginit:
+                raise NotImplementedError(f"{self.name}: input gradient would need accumulation")
+            self.vin.ensure_grad(n, e.tdtype, e.device)
+            dx = self.vin.gview(n)
+            if self.kind == "c3":
+                ops.conv3x3_dgrad(e.dt, dz, n, self.vout.h, self.vout.w, cout, self.w_bwd, self.cin, dx)
+            else:
+                if dx.ld != dx.c or dx.off:
+                    raise NotImplementedError("tconv input gradient into a concat slice")
+                ops.tconv_dgrad(e.dt, dz, n, self.vin.h, self.vin.w, cout, self.w_bwd, self.cin, dx.buf)
+            if self.vin.place:
+                self.vin.ginit = True  # only this slice was written
+            else:
+                self.vin.mark_grad()
+        self.r = None
+        self.cols = None
+
+
+class PoolStage(Stage):
+    def __init__(self, layer, vin, vout):
+        self.layer, self.vin, self.vout, self.name = layer, vin, vout, layer.name
+
+    def forward(self, n, training):
+        e = self.eng
+        if self.vout.place:
+            raise NotImplementedError("MaxPooling2D output feeding a concatenate")
+        self.vout.ensure(n, e.tdtype, e.device)
+        self.idx = torch.empty(n * self.vout.h * self.vout.w * self.vout.c, dtype=torch.uint8, device=e.device)
+        ops.maxpool_fwd(e.dt, self.vin.view(n), self.vout.buf, self.idx)
+
+    def backward(self, n):
+        e = self.eng
+        if not self.vin.needs_grad:
+            return
+        if not self.vin.ginit:
+            if self.vin.place:
+                raise NotImplementedError("pool gradient into an uninitialised concat slice")
+            self.vin.ensure_grad(n, e.tdtype, e.device, zero=True)
+        ops.maxpool_bwd(e.dt, self.vout.gbuf, self.idx, self.vin.gview(n))
+        self.idx = None
+
+
+class ConcatStage(Stage):
+    def __init__(self, layer, vins, vout):
+        self.layer, self.vins, self.vout, self.name = layer, vins, vout, layer.name
+
+    def forward(self, n, training):
+        self.vout.ensure(n, self.eng.tdtype, self.eng.device)
+
+    def backward(self, n):
+        pass
+
+
+class HeadStage(Stage):
+    def __init__(self, layer, vin):
+        self.layer, self.vin, self.name = layer, vin, layer.name
+        self.cin = vin.c
+        self.params = [(layer.name + "/kernel", (3, 1, 1, self.cin)), (layer.name + "/bias", (3,))]
+
+    def infer(self, n, yhat):
+        e = self.eng
+        ops.head_fwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
+                     e.p(self.name + "/bias"), yhat)
+
+    def loss_and_grad(self, n, target, loss_acc):
+        e = self.eng
+        self.vin.ensure_grad(n, e.tdtype, e.device)
+        rows = ops.head_rows(n * self.vin.h * self.vin.w)
+        part = torch.empty(rows * (5 + 3 * self.cin), device=e.device)
+        dx = self.vin.gview(n)
+        ops.head_fwd_bwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
+                         e.p(self.name + "/bias"), target, dx.buf, part)
+        ops.head_finalize(part, rows, self.cin, n * e.h_valid * self.vin.w * 3, loss_acc,
+                          e.g(self.name + "/kernel"), e.g(self.name + "/bias"))
+        self.vin.mark_grad()
+
+
+# ---------------------------------------------------------------------------
+def compile_graph(model):
+    """Turn the Keras layer graph into an ordered list of stages."""
+    layers = model.layers
+    cons = {}
+    for l in layers:
+        for t in l.inbound:
+            cons.setdefault(id(t), []).append(l)
+
+    def only_consumer(t):
+        c = cons.get(id(t), [])
+        return c[0] if len(c) == 1 else None
+
+    values = {}
+    stages = []
+    consumed = set()
+    inp = model.inputs[0]
+    vin = Value(inp.layer.name, inp.shape)
+    vin.needs_grad = False
+    values[id(inp)] = vin
+    drop_count = 0
+    out_t = model.outputs[0]
+    for l in layers:
+        if id(l) in consumed or isinstance(l, InputLayer):
+            continue
+        if isinstance(l, (Conv2D, Conv2DTranspose)):
+            x = l.inbound[0]
+            if isinstance(l, Conv2D) and l.kernel_size == (1, 1) and l.activation == "sigmoid":
+                if l.output is not out_t:
+                    raise NotImplementedError("a 1x1 sigmoid conv is supported only as the model head")
+                stages.append(HeadStage(l, values[id(x)]))
+                continue
+            if isinstance(l, Conv2D) and not (l.kernel_size == (3, 3) and l.padding == "same"):
+                raise NotImplementedError(f"{l.name}: only 3x3 'same' convs (and the 1x1 sigmoid head)")
+            t = l.output
+            relu = l.activation == "relu"
+            if l.activation not in (None, "relu"):
+                raise NotImplementedError(f"{l.name}: activation {l.activation}")
+            nxt = only_consumer(t)
+            if not relu and isinstance(nxt, Activation) and nxt.activation == "relu":
+                consumed.add(id(nxt))
+                relu = True
+                t = nxt.output
+                nxt = only_consumer(t)
+            if not relu:
+                raise NotImplementedError(f"{l.name}: conv without ReLU is not on the path")
+            bn = None
+            if isinstance(nxt, BatchNormalization):
+                bn = nxt
+                consumed.add(id(bn))
+                t = bn.output
+                nxt = only_consumer(t)
+            drop = None
+            drop_id = 0
+            if isinstance(nxt, Dropout):
+                if bn is None:
+                    raise NotImplementedError("Dropout without a preceding BatchNormalization")
+                drop = nxt
+                consumed.add(id(drop))
+                drop_count += 1
+                drop_id = drop_count  # ordinal of the Dropout in the model (1, 2): hash layer id
+                t = drop.output
+            if isinstance(l, Conv2DTranspose):
+                if bn is None:
+                    raise NotImplementedError("Conv2DTranspose without BN is not on the path")
+                kind = "t2"
+            elif x is inp and inp.shape[-1] == 3:
+                kind = "c3in"
+            else:
+                kind = "c3"
+            vout = Value(t.layer.name, t.shape)
+            values[id(t)] = vout
+            st = BlockStage(kind, l, relu, bn, drop, drop_id, values[id(x)], vout)
+            stages.append(st)
+        elif isinstance(l, MaxPooling2D):
+            vout = Value(l.name, l.output.shape)
+            values[id(l.output)] = vout
+            stages.append(PoolStage(l, values[id(l.inbound[0])], vout))
+        elif isinstance(l, Concatenate):
+            vout = Value(l.name, l.output.shape)
+            values[id(l.output)] = vout
+            off = 0
+            vins = []
+            for t in l.inbound:
+                v = values[id(t)]
+                if v.place is not None or v is vin or v.members:
+                    raise NotImplementedError(f"{l.name}: input {v.name} cannot be placed zero-copy")
+                v.place = (vout, off)
+                vout.members.append(v)
+                off += v.c
+                vins.append(v)
+            stages.append(ConcatStage(l, vins, vout))
+        else:
+            raise NotImplementedError(f"{l.name} ({type(l).__name__}) outside a fusable pattern")
+    if not stages or not isinstance(stages[-1], HeadStage):
+        raise NotImplementedError("the model must end in Conv2D(3, 1, activation='sigmoid')")
+    return stages
+
+
+class Engine:
+    """Runtime for one compiled model on one GPU (one process per GPU)."""
+
+    def __init__(self, model, dtype="float32", device="cuda"):
+        if not torch.cuda.is_available():
+            raise L.CnnItmoError("the CNN-ITMO engine needs a ROCm GPU (no CPU fallback)")
+        L.load()
+        self.model = model
+        self.dtype_name = dtype
+        self.dt, self.tdtype = ops.DTYPES[dtype]
+        self.device = torch.device(device)
+        self.stages = compile_graph(model)
+        self.h_valid = None
+        self.update_moving = True
+        self.drop_seed = 0
+        # flat parameter layout: reverse stage order
+        self.pslices, self.bslices = {}, {}
+        off = boff = 0
+        self.stage_goff = []  # per stage (in forward order): gradient range [lo, hi)
+        ranges = {}
+        for st in reversed(self.stages):
+            lo = off
+            for k, shp in st.params:
+                n = int(np.prod(shp))
+                self.pslices[k] = (off, shp)
+                off += -(-n // ALIGN) * ALIGN
+            ranges[id(st)] = (lo, off)
+            for k, shp in st.buffers:
+                n = int(np.prod(shp))
+                self.bslices[k] = (boff, shp)
+                boff += n
+        self.stage_goff = [ranges[id(s)] for s in self.stages]
+        self.nparams = off
+        self.params = torch.zeros(off, device=self.device)
+        self.grads = torch.zeros(off, device=self.device)
+        self.accum = torch.zeros(off, device=self.device)
+        self.bufs = torch.zeros(max(boff, 1), device=self.device)
+        for st in self.stages:
+            st.bind(self)
+        self.weights_dirty = True
+        self.step = 0
+        self.grad_hook = None  # callable(lo, hi) after each stage's gradients are written
+
+    # ---- parameter access ---------------------------------------------------
+    def _slice(self, flat, table, key):
+        off, shp = table[key]
+        return flat[off:off + int(np.prod(shp))]
+
+    def p(self, key):
+        return self._slice(self.params, self.pslices, key)
+
+    def g(self, key):
+        return self._slice(self.grads, self.pslices, key)
+
+    def b(self, key):
+        return self._slice(self.bufs, self.bslices, key)
+
+    def set_weights(self, named):
+        for k, v in named.items():
+            t = torch.as_tensor(np.ascontiguousarray(v, dtype=np.float32).reshape(-1))
+            if k in self.pslices:
+                self.p(k).copy_(t)
+            elif k in self.bslices:
+                self.b(k).copy_(t)
+            else:
+                raise KeyError(k)
+        self.weights_dirty = True
+
+    def get_weights(self):
+        out = {}
+        for k, (_, shp) in self.pslices.items():
+            out[k] = self.p(k).cpu().numpy().reshape(shp).copy()
+        for k, (_, shp) in self.bslices.items():
+            out[k] = self.b(k).cpu().numpy().reshape(shp).copy()
+        return out
+
+    def get_grads(self):
+        return {k: self.g(k).cpu().numpy().reshape(shp).copy() for k, (_, shp) in self.pslices.items()}
+
+    def prepare_weights(self):
+        if self.weights_dirty:
+            for st in self.stages:
+                if isinstance(st, BlockStage):
+                    st.prep()
+            self.weights_dirty = False
+
+    # ---- execution ----------------------------------------------------------
+    def _input(self, x):
+        """x: [n, h_valid, w, 3] fp32 device tensor; pads H to the model's height."""
+        n, hv, w, c = x.shape
+        vin = self.stages[0].vin if isinstance(self.stages[0], BlockStage) else None
+        H, W, C = self.model.inputs[0].shape
+        if c != 3 or w != W or hv > H or H - hv >= 16:
+            raise ValueError(f"input of shape {tuple(x.shape)} does not fit model input (None, {H}, {W}, {C})")
+        self.x_in = x.contiguous().float()
+        self.h_valid = hv
+        return n
+
+    def _release(self):
+        seen = set()
+        for st in self.stages:
+            for v in [getattr(st, "vout", None), getattr(st, "vin", None)] + list(getattr(st, "vins", [])):
+                if v is not None and id(v) not in seen:
+                    seen.add(id(v))
+                    v.release()
+
+    def forward(self, x, training=False):
+        n = self._input(x)
+        self.prepare_weights()
+        for st in self.stages[:-1]:
+            st.forward(n, training)
+        return n
+
+    def predict(self, x):
+        n = self.forward(x, training=False)
+        yhat = torch.empty(n, self.h_valid, self.model.inputs[0].shape[1], 3, device=self.device)
+        self.stages[-1].infer(n, yhat)
+        self._release()
+        return yhat
+
+    def train_step(self, x, target, seed=None, lr=1e-3, rho=0.9, eps=1e-7, grad_scale=1.0,
+                   sync=None, apply=True):
+        """One fwd+bwd+RMSprop step.  Returns a device tensor [loss, acc]."""
+        self.drop_seed = self.step if seed is None else int(seed)
+        n = self.forward(x, training=True)
+        loss_acc = torch.empty(2, device=self.device)
+        head = self.stages[-1]
+        head.loss_and_grad(n, target.contiguous().float(), loss_acc)
+        if self.grad_hook:
+            self.grad_hook(*self.stage_goff[-1])
+        for i in range(len(self.stages) - 2, -1, -1):
+            st = self.stages[i]
+            st.backward(n)
+            if self.grad_hook and st.params:
+                self.grad_hook(*self.stage_goff[i])
+        self._release()
+        if sync is not None:
+            sync()
+        if apply:
+            ops.rmsprop(self.params, self.grads, self.accum, lr, rho, eps, grad_scale)
+            self.weights_dirty = True
+        self.step += 1
+        return loss_acc
+
+    def evaluate_batch(self, x, target):
+        n = self.forward(x, training=False)
+        loss_acc = torch.empty(2, device=self.device)
+        saved = self.grads.clone()
+        self.stages[-1].loss_and_grad(n, target.contiguous().float(), loss_acc)
+        self.grads.copy_(saved)
+        self._release()
+        return loss_acc

@@ -355,10 +355,10 @@ class UNetRef:
         conv3 = cb("conv2d_6", cb("conv2d_5", pool2))
         pool3, c["pool3"] = maxpool2x2(conv3)
         conv4 = cb("conv2d_8", cb("conv2d_7", pool3))
-        drop4, c["keep4"] = drop(conv4, 4)
+        drop4, c["keep4"] = drop(conv4, 1)
         pool4, c["pool4"] = maxpool2x2(drop4)
         cross = cb("conv2d_10", cb("conv2d_9", pool4))
-        dropc, c["keepc"] = drop(cross, 10)
+        dropc, c["keepc"] = drop(cross, 2)
         up6 = tb("conv2d_transpose_1", dropc)
         conv6 = cb("conv2d_11", np.concatenate([drop4, up6], -1))
         up7 = tb("conv2d_transpose_2", conv6)

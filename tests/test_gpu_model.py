@@ -1,0 +1,239 @@
+"""End-to-end parity of the U-Net hot path on the GPU (HIP kernels via the C ABI)
+against the numpy oracle in fp64, same seeded weights and inputs.
+
+Tolerances (stated per north star):
+  fp32 inference: per-pixel max-abs <= 1e-4 and PSNR(gpu, target) within 0.01 dB
+  of PSNR(oracle, target).
+  fp32 training: loss rel <= 1e-5; the worst per-tensor gradient rel-L2 must be
+  no worse than that of numpy's own float32 run of the same oracle (and <= 2e-2).
+  Why self-calibrating: training-mode BN over near-degenerate channels (batch
+  variance << eps, e.g. conv2d_9 at 4x4x2 pixels) amplifies fp32 rounding ~30x
+  per layer, so fp32 gradients of this net are only ~1e-2 accurate against fp64
+  whoever computes them (tools/noise_floor.py); the per-kernel tests
+  (test_gpu_ops.py) pin every kernel at 1e-4 in isolation.  After one RMSprop
+  step the weights equal RMSprop applied to the GPU's own gradients (atol 1e-6).
+  bf16 (bf16 storage, fp32 accumulation): output max-abs <= 3e-2; one step: loss
+  rel <= 2e-2 and the head's gradients rel-L2 <= 0.1; functional: bf16 training
+  tracks fp32 training (final loss within 10%)."""
+import io
+import contextlib
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import unet_ref as R  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def build_unet(size, dtype, seed=1):
+    import cnn_itmo_amd as C
+    C.clear_session()
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = C.U_net(input_size=size, dtype=dtype, seed=seed)
+    return m
+
+
+def randomize_bn(m, rng):
+    named = m.named_weights()
+    upd = {}
+    for k, v in named.items():
+        if k.endswith("/moving_mean"):
+            upd[k] = rng.uniform(0, 1, v.shape)
+        elif k.endswith("/moving_variance"):
+            upd[k] = rng.uniform(0.5, 2, v.shape)
+        elif k.endswith("/gamma"):
+            upd[k] = rng.uniform(0.5, 1.5, v.shape)
+        elif k.endswith("/beta"):
+            upd[k] = rng.uniform(-0.2, 0.2, v.shape)
+        elif k.endswith("/bias"):
+            upd[k] = rng.uniform(-0.1, 0.1, v.shape)
+    m.set_named_weights(upd)
+    return m.named_weights()
+
+
+def psnr(a, b):
+    mse = float(np.mean((a - b) ** 2))
+    return 10 * np.log10(1.0 / mse) if mse > 0 else float("inf")
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_unet_inference_parity(dtype):
+    rng = np.random.default_rng(0)
+    m = build_unet((64, 64, 3), dtype)
+    P = randomize_bn(m, rng)
+    x = rng.integers(0, 256, size=(2, 64, 64, 3)) / 255.0
+    t = rng.uniform(size=x.shape)
+    y = m.predict(x)
+    ref = R.UNetRef(P).forward(x, training=False)
+    err = float(np.abs(y - ref).max())
+    if dtype == "float32":
+        assert err <= 1e-4, err
+        assert abs(psnr(y, t) - psnr(ref, t)) < 0.01
+    else:
+        assert err <= 3e-2, err
+
+
+def test_unet_inference_padded_1080_style():
+    """H not divisible by 16: pad=True model, zero-padded rows, cropped output."""
+    import cnn_itmo_amd as C
+    rng = np.random.default_rng(1)
+    C.clear_session()
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = C.U_net(input_size=(56, 48, 3), pad=True, seed=2)
+    assert m.input_shape == (None, 64, 48, 3)
+    P = randomize_bn(m, rng)
+    x = rng.uniform(size=(1, 56, 48, 3))
+    y = m.predict(x)
+    xp = np.zeros((1, 64, 48, 3))
+    xp[:, :56] = x
+    ref = R.UNetRef(P).forward(xp, training=False)[:, :56]
+    assert y.shape == (1, 56, 48, 3)
+    assert float(np.abs(y - ref).max()) <= 1e-4
+
+
+def _grad_err(g, r):
+    return float(np.abs(g - r).max()) / max(1e-12, float(np.abs(r).max()))
+
+
+def _rel_l2(g, r):
+    return float(np.linalg.norm(g - r)) / max(1e-12, float(np.linalg.norm(r)))
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_unet_train_step_parity(dtype):
+    rng = np.random.default_rng(2)
+    m = build_unet((64, 64, 3), dtype, seed=3)
+    P = randomize_bn(m, rng)
+    x = rng.integers(0, 256, size=(2, 64, 64, 3)) / 255.0
+    t = rng.uniform(size=x.shape)
+    eng = m._engine()
+    seed = 77
+    la = eng.train_step(torch.tensor(x, dtype=torch.float32).cuda(),
+                        torch.tensor(t, dtype=torch.float32).cuda(), seed=seed).cpu().numpy()
+    grads = eng.get_grads()
+    after = m.named_weights()
+    net = R.UNetRef(P)
+    net.forward(x, training=True, seed=seed)
+    loss, acc, rg = net.backward(t)
+    net.apply_rmsprop(rg, {})
+    assert set(rg) == set(grads)
+    if dtype == "float32":
+        assert abs(la[0] - loss) <= 1e-5 * loss
+        assert abs(la[1] - acc) <= 1.0 / x[..., 0].size + 1e-7
+        n32 = R.UNetRef(P, np.float32)
+        n32.forward(x.astype(np.float32), training=True, seed=seed)
+        _, _, g32 = n32.backward(t.astype(np.float32))
+        floor = max(_rel_l2(g32[k], rg[k]) for k in rg)
+        worst = max((_rel_l2(grads[k].reshape(rg[k].shape), rg[k]), k) for k in rg)
+        print(f"fp32 grad rel-L2: gpu worst {worst}, numpy-fp32 floor {floor:.3e}")
+        assert worst[0] <= min(2e-2, max(floor, 1e-3)), (worst, floor)
+        # optimizer wiring: weights after the step == RMSprop of the GPU's own gradients
+        for k in rg:
+            exp, _ = R.rmsprop(P[k].astype(np.float64), grads[k].reshape(P[k].shape).astype(np.float64),
+                               np.zeros(P[k].shape))
+            np.testing.assert_allclose(after[k], exp, atol=1e-6, err_msg=k)
+        for k in after:
+            if "moving" in k:
+                np.testing.assert_allclose(after[k], net.P[k], atol=1e-5, rtol=1e-5, err_msg=k)
+    else:
+        assert abs(la[0] - loss) <= 2e-2 * loss
+        for k in ("conv2d_15/kernel", "conv2d_15/bias", "batch_normalization_18/gamma",
+                  "batch_normalization_18/beta"):
+            assert _rel_l2(grads[k].reshape(rg[k].shape), rg[k]) <= 0.1, k
+
+
+def test_bf16_training_tracks_fp32():
+    """The bench dtype: 12 bf16 steps follow the fp32 loss trajectory."""
+    rng = np.random.default_rng(11)
+    x = rng.integers(0, 256, size=(4, 32, 32, 3)) / 255.0
+    t = np.clip(x ** 2.2 * 1.3, 0, 1)
+    curves = {}
+    for dtype in ("float32", "bfloat16"):
+        m = build_unet((32, 32, 3), dtype, seed=12)
+        eng = m._engine()
+        xs, ts = torch.tensor(x, dtype=torch.float32).cuda(), torch.tensor(t, dtype=torch.float32).cuda()
+        curves[dtype] = [eng.train_step(xs, ts, seed=i)[0].item() for i in range(12)]
+    f, b = curves["float32"], curves["bfloat16"]
+    assert f[-1] < f[0] and b[-1] < b[0], curves
+    assert abs(b[-1] - f[-1]) <= 0.1 * f[-1], curves
+
+
+def test_unet_two_steps_and_determinism():
+    """Two fp32 steps track the oracle; the same seeds give bitwise-equal results."""
+    rng = np.random.default_rng(4)
+    x = rng.uniform(size=(2, 32, 32, 3))
+    t = rng.uniform(size=x.shape)
+    outs = []
+    for _ in range(2):
+        m = build_unet((32, 32, 3), "float32", seed=5)
+        eng = m._engine()
+        xs, ts = torch.tensor(x, dtype=torch.float32).cuda(), torch.tensor(t, dtype=torch.float32).cuda()
+        l1 = eng.train_step(xs, ts, seed=1).cpu().numpy()
+        l2 = eng.train_step(xs, ts, seed=2).cpu().numpy()
+        outs.append((l1, l2, eng.params.cpu().numpy()))
+    assert np.array_equal(outs[0][2], outs[1][2])
+    P = build_unet((32, 32, 3), "float32", seed=5).named_weights()
+    net = R.UNetRef(P)
+    acc = {}
+    r1 = net.train_step(x, t, acc, seed=1)
+    r2 = net.train_step(x, t, acc, seed=2)
+    assert abs(outs[0][0][0] - r1[0]) <= 1e-5 * r1[0]
+    assert abs(outs[0][1][0] - r2[0]) <= 1e-3 * r2[0]
+
+
+def test_tiny_net_config1_parity():
+    """BASELINE configs[0]: 64x64, 3-conv net, batch 1 (fp32)."""
+    import cnn_itmo_amd as C
+    rng = np.random.default_rng(6)
+    C.clear_session()
+    m = C.TinyNet()
+    P = m.named_weights()
+    x = rng.uniform(size=(1, 64, 64, 3))
+    t = rng.uniform(size=x.shape)
+    y = m.predict(x)
+    ref = R.TinyNetRef(P)
+    assert float(np.abs(y - ref.forward(x)).max()) <= 1e-5
+    loss, acc, rg = ref.backward(t)
+    eng = m._engine()
+    la = eng.train_step(torch.tensor(x, dtype=torch.float32).cuda(), torch.tensor(t, dtype=torch.float32).cuda())
+    g = eng.get_grads()
+    assert abs(la[0].item() - loss) <= 1e-5 * loss
+    for k in rg:  # no BatchNorm here: well conditioned, tight tolerance
+        assert _grad_err(g[k].reshape(rg[k].shape), rg[k]) <= 1e-4, k
+
+
+def test_save_load_roundtrip(tmp_path):
+    import cnn_itmo_amd as C
+    rng = np.random.default_rng(7)
+    m = build_unet((32, 32, 3), "float32", seed=8)
+    x = rng.uniform(size=(1, 32, 32, 3))
+    m.train_on_batch(x, rng.uniform(size=x.shape))
+    y0 = m.predict(x)
+    p = str(tmp_path / "m.npz")
+    m.save(p)
+    m2 = C.load_model(p)
+    np.testing.assert_array_equal(m2.predict(x), y0)
+    assert m2.count_params() == m.count_params()
+
+
+def test_fit_generator_loss_decreases():
+    """main.py:126-132 shape of use: fit_generator over a paired generator."""
+    rng = np.random.default_rng(9)
+    m = build_unet((32, 32, 3), "float32", seed=10)
+    x = rng.uniform(size=(4, 32, 32, 3))
+    t = np.clip(x * 0.8 + 0.1, 0, 1)
+
+    def gen():
+        while True:
+            yield x[:2], t[:2]
+            yield x[2:], t[2:]
+    h = m.fit_generator(gen(), steps_per_epoch=10, epochs=3, verbose=0)
+    assert h.history["loss"][-1] < h.history["loss"][0]

@@ -169,8 +169,8 @@ def test_unet_full_grad_vs_torch():
     c1 = cb(cb(xi, "conv2d_1"), "conv2d_2")
     c2 = cb(cb(F.max_pool2d(c1, 2), "conv2d_3"), "conv2d_4")
     c3 = cb(cb(F.max_pool2d(c2, 2), "conv2d_5"), "conv2d_6")
-    c4 = drop(cb(cb(F.max_pool2d(c3, 2), "conv2d_7"), "conv2d_8"), 4)
-    cr = drop(cb(cb(F.max_pool2d(c4, 2), "conv2d_9"), "conv2d_10"), 10)
+    c4 = drop(cb(cb(F.max_pool2d(c3, 2), "conv2d_7"), "conv2d_8"), 1)
+    cr = drop(cb(cb(F.max_pool2d(c4, 2), "conv2d_9"), "conv2d_10"), 2)
     c6 = cb(torch.cat([c4, tb(cr, "conv2d_transpose_1")], 1), "conv2d_11")
     c7 = cb(torch.cat([c3, tb(c6, "conv2d_transpose_2")], 1), "conv2d_12")
     c8 = cb(torch.cat([c2, tb(c7, "conv2d_transpose_3")], 1), "conv2d_13")
