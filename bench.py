@@ -1,0 +1,291 @@
+#!/usr/bin/env python
+"""Benchmark: 1080p SDR->HDR U-Net training throughput on MI355X.
+
+BASELINE.json metric: "1080p SDR->HDR frames/sec (fwd+bwd) at 1/2/4/8 MI355X;
+MFMA % of peak".  Workload (BASELINE configs[2]/[3]): 1920x1080 frames padded to
+1920x1088 (the U-Net needs multiples of 16), batch 32 per GPU, bf16
+storage / fp32 accumulation, one step = forward + backward + RCCL gradient
+all-reduce (N>1) + RMSprop, synthetic data (uniform /255 inputs and targets),
+random-init weights of the reference architecture (model.py:204-281).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+Prints ONE JSON line on rank 0.  `value` = frames/s over all ranks (weak
+scaling: 32 frames per GPU per step).  `roofline` is for the dominant kernel,
+timed live with HIP events on the compute stream over the timed steps;
+`cpu_baseline` times this repo's numpy oracle (oracle/unet_ref.py) on the host.
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+BF16_PEAK_TF = 2516.6   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; spec ~2.5 PF dense)
+F32_PEAK_TF = 157.3     # MI355X fp32 MFMA (= fp32 vector rate)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32, help="frames per GPU")
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--dtype", default="bfloat16", choices=["bfloat16", "float32"])
+    ap.add_argument("--mode", default="train", choices=["train", "infer"])
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-scale", type=int, default=2, help="CPU sample = 1 frame at H/s x W/s")
+    ap.add_argument("--bucket-mb", type=float, default=16.0)
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------- kernel timing
+class KernelTimer:
+    """Brackets every launch of the implicit-GEMM conv kernels with HIP events on
+    the current (compute) stream and attributes algorithmic FLOPs to the kernel
+    instantiation that runs (same tile choice as csrc/igemm_fwd.hip:pick_cfg)."""
+
+    def __init__(self, ops, torch):
+        self.ops, self.torch = ops, torch
+        self.on = False
+        self.rec = []  # (name, flops, ev0, ev1)
+        self._wrap()
+
+    @staticmethod
+    def fwd_name(dt, n):
+        t = "bf16" if dt == 1 else "f32"
+        if n >= 128 and n % 128 == 0:
+            tile = "128x128"
+        elif n % 64 == 0:
+            tile = "256x64"
+        else:
+            tile = "256x32"
+        return f"igemm_fwd_kernel<{t},{tile}>"
+
+    def _bracket(self, name, flops, fn, *a, **k):
+        if not self.on:
+            return fn(*a, **k)
+        e0 = self.torch.cuda.Event(enable_timing=True)
+        e1 = self.torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn(*a, **k)
+        e1.record()
+        self.rec.append((name, flops, e0, e1))
+        return r
+
+    def _wrap(self):
+        ops = self.ops
+        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_dgrad", "tconv_fwd", "tconv_dgrad",
+                                           "conv1tap_fwd", "conv_wgrad", "tconv_wgrad")}
+
+        def conv3x3_fwd(dt, x, wt, bias, out, *a, **k):
+            fl = 2.0 * x.p * out.c * 9 * x.c
+            return self._bracket(self.fwd_name(dt, out.c), fl, o["conv3x3_fwd"], dt, x, wt, bias, out, *a, **k)
+
+        def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx):
+            fl = 2.0 * n * h * w * cin * 9 * cout
+            return self._bracket(self.fwd_name(dt, cin), fl, o["conv3x3_dgrad"], dt, dz, n, h, w, cout, wflip, cin, dx)
+
+        def tconv_fwd(dt, x, k_, bias, out, *a, **k):
+            fl = 2.0 * x.p * 4 * out.c * x.c
+            return self._bracket(self.fwd_name(dt, 4 * out.c), fl, o["tconv_fwd"], dt, x, k_, bias, out, *a, **k)
+
+        def tconv_dgrad(dt, dout, n, h, w, cout, kT, cin, dx):
+            fl = 2.0 * n * h * w * cin * 4 * cout
+            return self._bracket(self.fwd_name(dt, cin), fl, o["tconv_dgrad"], dt, dout, n, h, w, cout, kT, cin, dx)
+
+        def conv1tap_fwd(dt, cols, kk, m, wt, bias, out, *a, **k):
+            fl = 2.0 * m * out.c * 27  # algorithmic K = 3x3x3 (the packed 32 has 5 zero columns)
+            return self._bracket(self.fwd_name(dt, out.c), fl, o["conv1tap_fwd"], dt, cols, kk, m, wt, bias, out, *a, **k)
+
+        def conv_wgrad(dt, ntaps, x, dz, cout, dw, dw_cols=0):
+            fl = 2.0 * x.p * cout * (27 if ntaps == 1 else 9 * x.c)
+            t = "bf16" if dt == 1 else "f32"
+            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad_kernel + slab_reduce)", fl, o["conv_wgrad"],
+                                 dt, ntaps, x, dz, cout, dw, dw_cols)
+
+        def tconv_wgrad(dt, x, dout, cout, dk):
+            fl = 2.0 * x.p * 4 * cout * x.c
+            t = "bf16" if dt == 1 else "f32"
+            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad_kernel + slab_reduce)", fl, o["tconv_wgrad"],
+                                 dt, x, dout, cout, dk)
+
+        for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad), ("tconv_fwd", tconv_fwd),
+                     ("tconv_dgrad", tconv_dgrad), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),
+                     ("tconv_wgrad", tconv_wgrad)):
+            setattr(ops, n, f)
+
+    def summary(self):
+        agg = {}
+        for name, fl, e0, e1 in self.rec:
+            ms = e0.elapsed_time(e1)
+            a = agg.setdefault(name, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += fl
+            a[2] += ms
+        return agg
+
+
+# ---------------------------------------------------------------- CPU baseline
+def cpu_baseline(args, P_init, H, W):
+    """Time the numpy oracle (fp32, OpenBLAS sgemm) on one training step of ONE
+    frame at (H/s, W/s); report 1080p-frame-equivalents per second (FLOPs scale
+    with pixel count)."""
+    from oracle import unet_ref as R
+    s = args.cpu_scale
+    h, w = H // s, W // s
+    h, w = h - h % 16, w - w % 16
+    rng = np.random.default_rng(0)
+    x = (rng.integers(0, 256, size=(1, h, w, 3)) / 255.0).astype(np.float32)
+    t = (rng.integers(0, 256, size=(1, h, w, 3)) / 255.0).astype(np.float32)
+    net = R.UNetRef(P_init, np.float32)
+    t0 = time.perf_counter()
+    net.forward(x, training=True, seed=0)
+    net.backward(t)
+    dt = time.perf_counter() - t0
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("internal_api") in ("openblas", "mkl")] or [1])
+    except Exception:  # pragma: no cover
+        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    frac = (h * w) / float(H * W)
+    return {"value": frac / dt, "unit": "1080p frames/s (fwd+bwd, fp32)", "cores": threads, "kind": "port",
+            "sample": f"oracle/unet_ref.py numpy fp32 train step (fwd+bwd) on 1 frame {w}x{h} "
+                      f"({frac:.4f} of a 1920x{H} frame, scaled by pixel count); {dt:.2f} s",
+            "seconds": dt}
+
+
+def main():
+    args = parse()
+    import torch
+    from cnn_itmo_amd import dist as D
+    rank, world, local = D.init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    import cnn_itmo_amd as C
+    from cnn_itmo_amd import ops
+
+    H = -(-args.height // 16) * 16
+    W = -(-args.width // 16) * 16
+    with contextlib.redirect_stdout(io.StringIO()):
+        model = C.U_net(input_size=(args.height, args.width, 3), pad=True, dtype=args.dtype, seed=0,
+                        verbose=False)
+    P_init = model.named_weights() if rank == 0 else None
+    eng = model._engine()
+    bucketer = D.attach(eng, bucket_mb=args.bucket_mb) if world > 1 else None
+    timer = KernelTimer(ops, torch)
+
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + 7919 * rank)
+    B = args.batch
+    x = torch.randint(0, 256, (B, args.height, args.width, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+    t = torch.randint(0, 256, (B, args.height, args.width, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+    opt = model.optimizer
+
+    def step(i):
+        if args.mode == "infer":
+            eng.forward(x, training=False)
+            yhat = torch.empty(B, args.height, args.width, 3, device="cuda")
+            eng.stages[-1].infer(B, yhat)
+            eng._release()
+            return None
+        kw = dict(seed=i * 1000 + rank, lr=opt.lr, rho=opt.rho, eps=opt.epsilon)
+        if bucketer is not None:
+            kw.update(sync=bucketer.finish, grad_scale=bucketer.grad_scale)
+        return eng.train_step(x, t, **kw)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    timer.on = True
+    t0 = time.perf_counter()
+    losses = []
+    for i in range(args.steps):
+        losses.append(step(args.warmup + i))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    timer.on = False
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = el.item()
+    frames = B * world * args.steps
+    fps = frames / elapsed
+
+    agg = timer.summary()
+    dom = max(agg.items(), key=lambda kv: kv[1][2])
+    name, (cnt, fl, ms) = dom
+    peak = BF16_PEAK_TF if args.dtype == "bfloat16" else F32_PEAK_TF
+    achieved = fl / (ms * 1e-3) / 1e12
+    total_fl = sum(v[1] for v in agg.values())
+    total_ms = sum(v[2] for v in agg.values())
+    step_flops = total_fl / args.steps
+    if rank == 0:
+        for k, (c, f, m) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+            print(f"[bench] {k:55s} launches={c:5d} time={m:9.1f} ms  {f / (m * 1e-3) / 1e12:7.1f} TFLOP/s",
+                  file=sys.stderr)
+        if losses and losses[-1] is not None:
+            print(f"[bench] last loss/acc: {losses[-1].cpu().numpy().tolist()}", file=sys.stderr)
+        print(f"[bench] peak mem {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
+              f"step {elapsed / args.steps * 1e3:.1f} ms, conv share {total_ms / (elapsed * 1e3):.2%}",
+              file=sys.stderr)
+
+    traffic = None
+    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(name, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
+            "algorithmic_flop_per_launch": fl / cnt,
+            "step_conv_tflops": round(step_flops / (elapsed / args.steps) / 1e12, 2),
+            "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / peak, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "train":
+        try:
+            cpu = cpu_baseline(args, P_init, H, W)
+        except Exception as e:  # report, never fail the bench on the CPU leg
+            cpu = {"error": repr(e)}
+
+    if rank == 0:
+        metric = "1080p SDR->HDR frames/sec (fwd+bwd)" if args.mode == "train" else "1080p SDR->HDR frames/sec (fwd)"
+        line = {"metric": metric, "value": round(fps, 3), "unit": "frames/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "bf16" if args.dtype == "bfloat16" else "f32", "data": "synthetic",
+                "config": {"workload": f"U-Net (model.py:204) {args.mode} step, {args.width}x{args.height} "
+                                       f"frames padded to {W}x{H}, {B} frames/GPU",
+                           "global_batch": B * world, "frame": [args.height, args.width],
+                           "padded": [H, W], "parallelism": f"dp{world}",
+                           "gflop_per_frame": round(step_flops / B / 1e9, 1)},
+                "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -401,6 +401,26 @@ def compile_graph(model):
     return stages
 
 
+def layout_params(stages):
+    """Flat fp32 layout of every trainable tensor in REVERSE stage order (backward
+    writes gradients front to back).  Returns (pslices, bslices, stage_goff,
+    nparams, nbuffers); stage_goff[i] = [lo, hi) gradient range of stages[i]."""
+    pslices, bslices, ranges = {}, {}, {}
+    off = boff = 0
+    for st in reversed(stages):
+        lo = off
+        for k, shp in st.params:
+            n = int(np.prod(shp))
+            pslices[k] = (off, shp)
+            off += -(-n // ALIGN) * ALIGN
+        ranges[id(st)] = (lo, off)
+        for k, shp in st.buffers:
+            n = int(np.prod(shp))
+            bslices[k] = (boff, shp)
+            boff += n
+    return pslices, bslices, [ranges[id(s)] for s in stages], off, boff
+
+
 class Engine:
     """Runtime for one compiled model on one GPU (one process per GPU)."""
 
@@ -416,23 +436,7 @@ class Engine:
         self.h_valid = None
         self.update_moving = True
         self.drop_seed = 0
-        # flat parameter layout: reverse stage order
-        self.pslices, self.bslices = {}, {}
-        off = boff = 0
-        self.stage_goff = []  # per stage (in forward order): gradient range [lo, hi)
-        ranges = {}
-        for st in reversed(self.stages):
-            lo = off
-            for k, shp in st.params:
-                n = int(np.prod(shp))
-                self.pslices[k] = (off, shp)
-                off += -(-n // ALIGN) * ALIGN
-            ranges[id(st)] = (lo, off)
-            for k, shp in st.buffers:
-                n = int(np.prod(shp))
-                self.bslices[k] = (boff, shp)
-                boff += n
-        self.stage_goff = [ranges[id(s)] for s in self.stages]
+        self.pslices, self.bslices, self.stage_goff, off, boff = layout_params(self.stages)
         self.nparams = off
         self.params = torch.zeros(off, device=self.device)
         self.grads = torch.zeros(off, device=self.device)
