@@ -199,7 +199,7 @@ def main():
     def step(i):
         if args.mode == "infer":
             eng.forward(x, training=False)
-            yhat = torch.empty(B, args.height, args.width, 3, device="cuda")
+            yhat = torch.empty(B, args.height, args.width, 3, device="cuda", dtype=torch.float32)
             eng.stages[-1].infer(B, yhat)
             eng._release()
             return None

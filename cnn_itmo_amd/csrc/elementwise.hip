@@ -68,11 +68,19 @@ static int colsum_stage1_launch(const float* part, long rows, int cols, void* ws
   return G;
 }
 
+// Fold the G stage-1 rows of one column with a whole wave (fixed-order tree:
+// deterministic).  Every lane returns the total.  Finalize kernels run one
+// 64-lane wave per output column (256-thread blocks = 4 columns).
 __device__ __forceinline__ double fold(const double* ws, int G, int cols, int col) {
+  const int lane = threadIdx.x & 63;
   double s = 0.0;
-  for (int g = 0; g < G; ++g) s += ws[(size_t)g * cols + col];
+  for (int g = lane; g < G; g += 64) s += ws[(size_t)g * cols + col];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   return s;
 }
+__device__ __forceinline__ int wave_col() { return blockIdx.x * 4 + (threadIdx.x >> 6); }
+static inline int wave_grid(int ncols) { return (ncols + 3) / 4; }
 
 extern "C" size_t cnnitmo_reduce_workspace_bytes(long rows, int cols) {
   return (size_t)red_groups(rows) * cols * sizeof(double);
@@ -80,12 +88,12 @@ extern "C" size_t cnnitmo_reduce_workspace_bytes(long rows, int cols) {
 
 __global__ void colsum_final(const double* __restrict__ ws, int G, int cols, int groups,
                              float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = wave_col();
   const int C = cols / groups;
   if (c >= C) return;
   double s = 0.0;
   for (int gr = 0; gr < groups; ++gr) s += fold(ws, G, cols, gr * C + c);
-  out[c] = (float)s;
+  if ((threadIdx.x & 63) == 0) out[c] = (float)s;
 }
 
 extern "C" int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* out,
@@ -94,7 +102,7 @@ extern "C" int cnnitmo_colsum(const float* part, long rows, int cols, int groups
   hipStream_t s = (hipStream_t)stream;
   const int G = colsum_stage1_launch(part, rows, cols, workspace, s);
   const int C = cols / groups;
-  hipLaunchKernelGGL(colsum_final, dim3((C + 255) / 256), dim3(256), 0, s,
+  hipLaunchKernelGGL(colsum_final, dim3(wave_grid(C)), dim3(256), 0, s,
                      (const double*)workspace, G, cols, groups, out);
   return cnnitmo_check_launch("colsum");
 }
@@ -108,7 +116,7 @@ __global__ void bn_fwd_final_kernel(const double* __restrict__ ws, int G, int C,
                                     const float* __restrict__ beta, float* mm, float* mv,
                                     float momentum, float eps, float* scale, float* shift,
                                     float* smean, float* sinv) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = wave_col();
   if (c >= C) return;
   const int cols = 2 * groups * C;
   double s1 = 0.0, s2 = 0.0;
@@ -120,6 +128,7 @@ __global__ void bn_fwd_final_kernel(const double* __restrict__ ws, int G, int C,
   const double var = fmax(s2 / count - mean * mean, 0.0);  // biased (tf.nn.moments)
   const double inv = 1.0 / sqrt(var + (double)eps);
   const double sc = (double)gamma[c] * inv;
+  if ((threadIdx.x & 63) != 0) return;
   scale[c] = (float)sc;
   shift[c] = (float)((double)beta[c] - mean * sc);
   smean[c] = (float)mean;
@@ -140,7 +149,7 @@ extern "C" int cnnitmo_bn_fwd_finalize(const float* stat_part, long rows, int c,
   CNN_REQUIRE(rows > 0 && c > 0 && groups >= 1 && count > 1.0, "bn_fwd_finalize: bad sizes");
   hipStream_t s = (hipStream_t)stream;
   const int G = colsum_stage1_launch(stat_part, rows, 2 * groups * c, workspace, s);
-  hipLaunchKernelGGL(bn_fwd_final_kernel, dim3((c + 255) / 256), dim3(256), 0, s,
+  hipLaunchKernelGGL(bn_fwd_final_kernel, dim3(wave_grid(c)), dim3(256), 0, s,
                      (const double*)workspace, G, c, groups, count, gamma, beta, moving_mean,
                      moving_var, momentum, eps, scale, shift, save_mean, save_invstd);
   return cnnitmo_check_launch("bn_fwd_finalize");
@@ -305,9 +314,10 @@ __global__ void bn_bwd_final_kernel(const double* __restrict__ ws, int G, int C,
                                     const float* __restrict__ gamma, const float* __restrict__ mean,
                                     const float* __restrict__ inv, float* dgamma, float* dbeta,
                                     float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = wave_col();
   if (c >= C) return;
   const double sdy = fold(ws, G, 2 * C, c), sdyr = fold(ws, G, 2 * C, C + c);
+  if ((threadIdx.x & 63) != 0) return;
   if (dgamma) dgamma[c] = (float)sdyr;
   if (dbeta) dbeta[c] = (float)sdy;
   const double a = (double)gamma[c] * inv[c];
@@ -324,7 +334,7 @@ extern "C" int cnnitmo_bn_bwd_finalize(const float* part, long rows, int c, doub
                                        void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int G = colsum_stage1_launch(part, rows, 2 * c, workspace, s);
-  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((c + 255) / 256), dim3(256), 0, s,
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(wave_grid(c)), dim3(256), 0, s,
                      (const double*)workspace, G, c, count, gamma, mean, invstd, dgamma, dbeta, coef);
   return cnnitmo_check_launch("bn_bwd_finalize");
 }
@@ -659,8 +669,10 @@ extern "C" int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int 
 __global__ void head_final_kernel(const double* __restrict__ ws, int G, int cin, double numel,
                                   float* loss_acc, float* dw, float* db) {
   const int ncol = 5 + 3 * cin;
-  for (int k = threadIdx.x; k < ncol; k += blockDim.x) {
+  const int k = wave_col();
+  if (k < ncol) {
     const double s = fold(ws, G, ncol, k);
+    if ((threadIdx.x & 63) != 0) return;
     if (k == 0) loss_acc[0] = (float)(s / numel);
     else if (k == 1) loss_acc[1] = (float)(s / (numel / 3.0));
     else if (k < 5) db[k - 2] = (float)s;
@@ -673,7 +685,7 @@ extern "C" int cnnitmo_head_finalize(const float* part, long rows, int cin, doub
                                      void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int G = colsum_stage1_launch(part, rows, 5 + 3 * cin, workspace, s);
-  hipLaunchKernelGGL(head_final_kernel, dim3(1), dim3(256), 0, s, (const double*)workspace, G, cin,
+  hipLaunchKernelGGL(head_final_kernel, dim3(wave_grid(5 + 3 * cin)), dim3(256), 0, s, (const double*)workspace, G, cin,
                      numel, loss_acc, dw, db);
   return cnnitmo_check_launch("head_finalize");
 }

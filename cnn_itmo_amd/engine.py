@@ -170,21 +170,21 @@ class BlockStage(Stage):
         g, b = e.p(bn.name + "/gamma"), e.p(bn.name + "/beta")
         mm, mv = e.b(bn.name + "/moving_mean"), e.b(bn.name + "/moving_variance")
         if not training:
-            sc = torch.empty(cout, device=e.device)
-            sh = torch.empty(cout, device=e.device)
+            sc = torch.empty(cout, device=e.device, dtype=torch.float32)
+            sh = torch.empty(cout, device=e.device, dtype=torch.float32)
             ops.bn_infer_coeffs(cout, g, b, mm, mv, bn.epsilon, sc, sh)
             self._conv(n, out, (L.RELU if self.relu else 0) | L.AFFINE, aff=(sc, sh))
             return
         m, ncols = self._gemm_rows(n)
         rows = ops.fwd_stat_rows(e.dt, m, ncols)
-        stats = torch.empty(rows * 2 * ncols, device=e.device)
+        stats = torch.empty(rows * 2 * ncols, device=e.device, dtype=torch.float32)
         r = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
         self._conv(n, ops.View(r, n, self.vout.h, self.vout.w, cout, cout, 0),
                    (L.RELU if self.relu else 0) | L.STATS, stats=stats)
-        self.scale = torch.empty(cout, device=e.device)
-        self.shift = torch.empty(cout, device=e.device)
-        self.smean = torch.empty(cout, device=e.device)
-        self.sinv = torch.empty(cout, device=e.device)
+        self.scale = torch.empty(cout, device=e.device, dtype=torch.float32)
+        self.shift = torch.empty(cout, device=e.device, dtype=torch.float32)
+        self.smean = torch.empty(cout, device=e.device, dtype=torch.float32)
+        self.sinv = torch.empty(cout, device=e.device, dtype=torch.float32)
         ops.bn_fwd_finalize(stats, rows, cout, 4 if self.kind == "t2" else 1, P, g, b,
                             mm if e.update_moving else None, mv if e.update_moving else None,
                             bn.momentum, bn.epsilon, self.scale, self.shift, self.smean, self.sinv)
@@ -201,14 +201,14 @@ class BlockStage(Stage):
         dy = self.vout.gview(n)
         rows = ops.bn_bwd_rows(P, cout)
         dz = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
-        part2 = torch.empty(rows * cout, device=e.device)
+        part2 = torch.empty(rows * cout, device=e.device, dtype=torch.float32)
         flags = L.DROPOUT if self.drop is not None else 0
         if self.bn is not None:
             bn = self.bn
-            part = torch.empty(rows * 2 * cout, device=e.device)
+            part = torch.empty(rows * 2 * cout, device=e.device, dtype=torch.float32)
             ops.bn_bwd_reduce(e.dt, dy, self.r, cout, self.smean, self.sinv, flags, e.drop_seed,
                               self.drop_id, part)
-            coef = torch.empty(3 * cout, device=e.device)
+            coef = torch.empty(3 * cout, device=e.device, dtype=torch.float32)
             ops.bn_bwd_finalize(part, rows, cout, P, e.p(bn.name + "/gamma"), self.smean, self.sinv,
                                 e.g(bn.name + "/gamma"), e.g(bn.name + "/beta"), coef)
             ops.bn_bwd_apply(e.dt, dy, self.r, cout, coef, flags, e.drop_seed, self.drop_id, dz, part2)
@@ -293,7 +293,7 @@ class HeadStage(Stage):
         e = self.eng
         self.vin.ensure_grad(n, e.tdtype, e.device)
         rows = ops.head_rows(n * self.vin.h * self.vin.w)
-        part = torch.empty(rows * (5 + 3 * self.cin), device=e.device)
+        part = torch.empty(rows * (5 + 3 * self.cin), device=e.device, dtype=torch.float32)
         dx = self.vin.gview(n)
         ops.head_fwd_bwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
                          e.p(self.name + "/bias"), target, dx.buf, part)
@@ -438,10 +438,10 @@ class Engine:
         self.drop_seed = 0
         self.pslices, self.bslices, self.stage_goff, off, boff = layout_params(self.stages)
         self.nparams = off
-        self.params = torch.zeros(off, device=self.device)
-        self.grads = torch.zeros(off, device=self.device)
-        self.accum = torch.zeros(off, device=self.device)
-        self.bufs = torch.zeros(max(boff, 1), device=self.device)
+        self.params = torch.zeros(off, device=self.device, dtype=torch.float32)
+        self.grads = torch.zeros(off, device=self.device, dtype=torch.float32)
+        self.accum = torch.zeros(off, device=self.device, dtype=torch.float32)
+        self.bufs = torch.zeros(max(boff, 1), device=self.device, dtype=torch.float32)
         for st in self.stages:
             st.bind(self)
         self.weights_dirty = True
@@ -520,7 +520,7 @@ class Engine:
 
     def predict(self, x):
         n = self.forward(x, training=False)
-        yhat = torch.empty(n, self.h_valid, self.model.inputs[0].shape[1], 3, device=self.device)
+        yhat = torch.empty(n, self.h_valid, self.model.inputs[0].shape[1], 3, device=self.device, dtype=torch.float32)
         self.stages[-1].infer(n, yhat)
         self._release()
         return yhat
@@ -530,7 +530,7 @@ class Engine:
         """One fwd+bwd+RMSprop step.  Returns a device tensor [loss, acc]."""
         self.drop_seed = self.step if seed is None else int(seed)
         n = self.forward(x, training=True)
-        loss_acc = torch.empty(2, device=self.device)
+        loss_acc = torch.empty(2, device=self.device, dtype=torch.float32)
         head = self.stages[-1]
         head.loss_and_grad(n, target.contiguous().float(), loss_acc)
         if self.grad_hook:
@@ -551,7 +551,7 @@ class Engine:
 
     def evaluate_batch(self, x, target):
         n = self.forward(x, training=False)
-        loss_acc = torch.empty(2, device=self.device)
+        loss_acc = torch.empty(2, device=self.device, dtype=torch.float32)
         saved = self.grads.clone()
         self.stages[-1].loss_and_grad(n, target.contiguous().float(), loss_acc)
         self.grads.copy_(saved)

@@ -8,11 +8,11 @@ import torch.nn.functional as F
 
 from oracle import unet_ref as R
 
-torch.set_default_dtype(torch.float64)
+
 
 
 def t(a, grad=False):
-    x = torch.tensor(np.asarray(a, np.float64))
+    x = torch.tensor(np.asarray(a, np.float64), dtype=torch.float64)
     x.requires_grad_(grad)
     return x
 
@@ -160,7 +160,7 @@ def test_unet_full_grad_vs_torch():
 
     def drop(y, layer):
         keep = R.dropout_keep(11, layer, y.numel()).reshape(y.shape[0], y.shape[2], y.shape[3], y.shape[1])
-        m = torch.tensor(keep.astype(np.float64)).permute(0, 3, 1, 2)
+        m = torch.tensor(keep.astype(np.float64), dtype=torch.float64).permute(0, 3, 1, 2)
         return y * m * 2
 
     cb = lambda xx, n: bnrelu(conv(xx, n), n)
