@@ -19,6 +19,8 @@ STATS = 2
 AFFINE = 4
 DROPOUT = 1
 NO_BN = 2
+PARITY = 4
+BIAS_PER_COL = 8
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -32,35 +34,39 @@ sz = C.c_size_t
 SIGNATURES = {
     "cnnitmo_version": (i32, []),
     "cnnitmo_last_error": (C.c_char_p, []),
-    "cnnitmo_conv3x3_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
+    "cnnitmo_conv3x3_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp]),
     "cnnitmo_fwd_stat_rows": (i32, [i32, i64, i32]),
     "cnnitmo_conv3x3_dgrad": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, vp]),
     "cnnitmo_wgrad_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32, i32]),
-    "cnnitmo_conv_wgrad": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, vp, i32, vp, sz, vp]),
+    "cnnitmo_conv_wgrad": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
     "cnnitmo_im2col_c3": (i32, [i32, vp, i32, i32, i32, i32, vp, vp]),
     "cnnitmo_conv1tap_fwd": (i32, [i32, vp, i32, i64, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_tconv2x2_fwd": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_tconv2x2_dgrad": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, vp]),
-    "cnnitmo_tconv2x2_wgrad": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, sz, vp]),
+    "cnnitmo_tconv2x2_wgrad": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz, vp]),
     "cnnitmo_tconv2x2_wgrad_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32]),
     "cnnitmo_prep_conv3x3_weights": (i32, [i32, vp, i32, i32, vp, vp, vp]),
     "cnnitmo_prep_tconv2x2_weights": (i32, [i32, vp, i32, i32, vp, vp, vp]),
     "cnnitmo_prep_c3_weights": (i32, [i32, vp, i32, vp, vp]),
-    "cnnitmo_maxpool2x2_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "cnnitmo_maxpool2x2_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp]),
     "cnnitmo_maxpool2x2_bwd": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, vp]),
     "cnnitmo_reduce_workspace_bytes": (sz, [i64, i32]),
     "cnnitmo_bn_fwd_finalize": (i32, [vp, i64, i32, i32, f64, vp, vp, vp, vp, f32, f32, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_bn_infer_coeffs": (i32, [i32, vp, vp, vp, vp, f32, vp, vp, vp]),
     "cnnitmo_bn_apply": (i32, [i32, vp, i64, i32, vp, vp, vp, i32, i32, i32, u64, i32, vp]),
     "cnnitmo_bn_bwd_rows": (i32, [i64, i32]),
-    "cnnitmo_bn_bwd_reduce": (i32, [i32, vp, i32, i32, vp, i64, i32, vp, vp, i32, u64, i32, vp, vp]),
+    "cnnitmo_bn_bwd_reduce": (i32, [i32, vp, i32, i32, vp, i32, i32, i64, i32, vp, vp, i32, u64, i32, vp, vp]),
     "cnnitmo_bn_bwd_finalize": (i32, [vp, i64, i32, f64, vp, vp, vp, vp, vp, vp, vp, vp]),
-    "cnnitmo_bn_bwd_apply": (i32, [i32, vp, i32, i32, vp, i64, i32, vp, i32, u64, i32, vp, vp, vp]),
+    "cnnitmo_bn_bwd_apply": (i32, [i32, vp, i32, i32, vp, i32, i32, i64, i32, vp, i32, u64, i32, i32, i32, vp, vp, vp]),
     "cnnitmo_colsum": (i32, [vp, i64, i32, i32, vp, vp, vp]),
-    "cnnitmo_head_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+    "cnnitmo_head_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_head_rows": (i32, [i64]),
-    "cnnitmo_head_fwd_bwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
-    "cnnitmo_head_finalize": (i32, [vp, i64, i32, f64, vp, vp, vp, vp, vp]),
+    "cnnitmo_head_fwd_bwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "cnnitmo_head_finalize": (i32, [vp, i64, i32, f64, vp, vp, vp, vp, vp, vp, vp]),
+    "cnnitmo_fold_conv3x3": (i32, [i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
+    "cnnitmo_fold_tconv2x2": (i32, [i32, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
+    "cnnitmo_border_rows": (i32, [i32]),
+    "cnnitmo_border_sums": (i32, [i32, vp, i32, i32, i32, i32, vp, vp]),
     "cnnitmo_rmsprop": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, vp]),
 }
 

@@ -258,7 +258,7 @@ __device__ void block_reduce_rows(float (&acc)[NS][VE], int C, float* __restrict
 
 template <typename T>
 __global__ void bn_bwd_reduce_kernel(const T* __restrict__ dy, long dy_ld, int dy_off,
-                                     const T* __restrict__ r, long P, int C,
+                                     const T* __restrict__ r, long r_ld, int r_off, long P, int C,
                                      const float* __restrict__ mean, const float* __restrict__ inv,
                                      int drop, uint64_t dbase, float* __restrict__ part) {
   constexpr int VE = Vec16<T>::N;
@@ -278,7 +278,7 @@ __global__ void bn_bwd_reduce_kernel(const T* __restrict__ dy, long dy_ld, int d
     for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
       float g[VE], rv[VE];
       load_dy<T>(dy, dy_ld, dy_off, p, C, c0, drop, dbase, g);
-      Pack16<T>::load(r + (size_t)p * C + c0, rv);
+      Pack16<T>::load(r + (size_t)p * r_ld + r_off + c0, rv);
 #pragma unroll
       for (int e = 0; e < VE; ++e) {
         acc[0][e] += g[e];
@@ -290,7 +290,7 @@ __global__ void bn_bwd_reduce_kernel(const T* __restrict__ dy, long dy_ld, int d
 }
 
 extern "C" int cnnitmo_bn_bwd_reduce(int dtype, const void* dy, int dy_ld, int dy_off,
-                                     const void* r, long p, int c, const float* mean,
+                                     const void* r, int r_ld, int r_off, long p, int c, const float* mean,
                                      const float* invstd, int flags, uint64_t drop_seed,
                                      int drop_layer, float* part, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -298,14 +298,14 @@ extern "C" int cnnitmo_bn_bwd_reduce(int dtype, const void* dy, int dy_ld, int d
   const int drop = (flags & CNNITMO_DROPOUT) ? 1 : 0;
   const uint64_t base = dropout_base(drop_seed, (uint64_t)drop_layer);
   const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
-  CNN_REQUIRE(c % VE == 0 && c / VE <= 256 && dy_ld % VE == 0 && dy_off % VE == 0,
-              "bn_bwd_reduce: unsupported channel count %d", c);
+  CNN_REQUIRE(c % VE == 0 && c / VE <= 256 && dy_ld % VE == 0 && dy_off % VE == 0 &&
+              r_ld % VE == 0 && r_off % VE == 0, "bn_bwd_reduce: unsupported channel count %d", c);
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dy,
-                       (long)dy_ld, dy_off, (const bf16*)r, p, c, mean, invstd, drop, base, part);
+                       (long)dy_ld, dy_off, (const bf16*)r, (long)r_ld, r_off, p, c, mean, invstd, drop, base, part);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dy,
-                       (long)dy_ld, dy_off, (const float*)r, p, c, mean, invstd, drop, base, part);
+                       (long)dy_ld, dy_off, (const float*)r, (long)r_ld, r_off, p, c, mean, invstd, drop, base, part);
   return cnnitmo_check_launch("bn_bwd_reduce");
 }
 
@@ -339,20 +339,25 @@ extern "C" int cnnitmo_bn_bwd_finalize(const float* part, long rows, int c, doub
   return cnnitmo_check_launch("bn_bwd_finalize");
 }
 
-template <typename T>
+// NP = 1: partial sums of dz per channel (bias gradient); NP = 4: split by the
+// pixel's (h&1, w&1) parity, i.e. per Conv2DTranspose tap of the producer
+// (needed by the folded-BN wgrad correction of the tconv; db = their sum).
+template <typename T, int NP>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, long dy_ld, int dy_off,
-                                    const T* __restrict__ r, long P, int C,
+                                    const T* __restrict__ r, long r_ld, int r_off, long P, int C,
                                     const float* __restrict__ coef, int nobn, int drop,
-                                    uint64_t dbase, T* __restrict__ dz, float* __restrict__ part) {
+                                    uint64_t dbase, T* __restrict__ dz, float* __restrict__ part,
+                                    int H, int W) {
   constexpr int VE = Vec16<T>::N;
   const int tpp = C / VE, rows = 256 / tpp;
   const int tid = threadIdx.x;
   const int row = tid / tpp, cv = tid - row * tpp, c0 = cv * VE;
-  float acc[1][VE];
+  float acc[NP][VE];
   float ca[VE], cb[VE], ce[VE];
 #pragma unroll
   for (int e = 0; e < VE; ++e) {
-    acc[0][e] = 0.f;
+#pragma unroll
+    for (int k = 0; k < NP; ++k) acc[k][e] = 0.f;
     const bool ok = row < rows && !nobn;
     ca[e] = ok ? coef[c0 + e] : 1.f;
     cb[e] = ok ? coef[C + c0 + e] : 0.f;
@@ -362,41 +367,56 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, long dy_ld, int dy
     for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
       float g[VE], rv[VE];
       load_dy<T>(dy, dy_ld, dy_off, p, C, c0, drop, dbase, g);
-      Pack16<T>::load(r + (size_t)p * C + c0, rv);
+      Pack16<T>::load(r + (size_t)p * r_ld + r_off + c0, rv);
 #pragma unroll
       for (int e = 0; e < VE; ++e) {
         const float d = rv[e] > 0.f ? (ca[e] * g[e] - cb[e] * rv[e] + ce[e]) : 0.f;
         g[e] = d;
       }
       Pack16<T>::store(dz + (size_t)p * C + c0, g);
+      int k = 0;
+      if constexpr (NP == 4) {
+        const int rem = (int)(p % ((long)H * W));
+        const int hh = rem / W, ww = rem - hh * W;
+        k = ((hh & 1) << 1) | (ww & 1);
+      }
       // bias gradient from the stored (rounded) dz, as the weight gradient sees it
 #pragma unroll
-      for (int e = 0; e < VE; ++e) acc[0][e] += to_f32(from_f32<T>(g[e]));
+      for (int kk = 0; kk < NP; ++kk)
+        if (kk == k) {
+#pragma unroll
+          for (int e = 0; e < VE; ++e) acc[kk][e] += to_f32(from_f32<T>(g[e]));
+        }
     }
   }
-  block_reduce_rows<VE, 1>(acc, C, part);
+  block_reduce_rows<VE, NP>(acc, C, part);
 }
 
 extern "C" int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off,
-                                    const void* r, long p, int c, const float* coef, int flags,
-                                    uint64_t drop_seed, int drop_layer, void* dz, float* part,
-                                    void* stream) {
+                                    const void* r, int r_ld, int r_off, long p, int c,
+                                    const float* coef, int flags, uint64_t drop_seed, int drop_layer,
+                                    int h, int w, void* dz, float* part, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int G = cnnitmo_bn_bwd_rows(p, c);
   const int drop = (flags & CNNITMO_DROPOUT) ? 1 : 0;
   const int nobn = (flags & CNNITMO_NO_BN) ? 1 : 0;
   const uint64_t base = dropout_base(drop_seed, (uint64_t)drop_layer);
   const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
-  CNN_REQUIRE(c % VE == 0 && c / VE <= 256 && dy_ld % VE == 0 && dy_off % VE == 0,
-              "bn_bwd_apply: unsupported channel count %d", c);
+  CNN_REQUIRE(c % VE == 0 && c / VE <= 256 && dy_ld % VE == 0 && dy_off % VE == 0 &&
+              r_ld % VE == 0 && r_off % VE == 0, "bn_bwd_apply: unsupported channel count %d", c);
   CNN_REQUIRE(nobn || coef, "bn_bwd_apply: missing coefficients");
-  if (dtype == CNNITMO_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dy,
-                       (long)dy_ld, dy_off, (const bf16*)r, p, c, coef, nobn, drop, base, (bf16*)dz, part);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dy,
-                       (long)dy_ld, dy_off, (const float*)r, p, c, coef, nobn, drop, base, (float*)dz,
-                       part);
+  const bool par = flags & CNNITMO_PARITY;
+  CNN_REQUIRE(!par || (h > 0 && w > 0), "bn_bwd_apply: PARITY needs h, w");
+#define BNA(T, NP)                                                                                \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, NP>), dim3(G), dim3(256), 0, s, (const T*)dy,        \
+                     (long)dy_ld, dy_off, (const T*)r, (long)r_ld, r_off, p, c, coef, nobn, drop, \
+                     base, (T*)dz, part, h, w)
+  if (dtype == CNNITMO_BF16) {
+    if (par) BNA(bf16, 4); else BNA(bf16, 1);
+  } else {
+    if (par) BNA(float, 4); else BNA(float, 1);
+  }
+#undef BNA
   return cnnitmo_check_launch("bn_bwd_apply");
 }
 
@@ -406,7 +426,8 @@ extern "C" int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy
 // ----------------------------------------------------------------------------
 template <typename T>
 __global__ void maxpool_fwd_kernel(const T* __restrict__ x, long x_ld, int x_off, int N, int H,
-                                   int W, int C, T* __restrict__ y, uint8_t* __restrict__ idx) {
+                                   int W, int C, T* __restrict__ y, uint8_t* __restrict__ idx,
+                                   const float* __restrict__ sc, const float* __restrict__ sh) {
   constexpr int VE = Vec16<T>::N;
   const int Ho = H / 2, Wo = W / 2, cv = C / VE;
   const long total = (long)N * Ho * Wo * cv;
@@ -424,6 +445,10 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, long x_ld, int x_off
       const long pin = ((long)n * H + 2 * ho + (k >> 1)) * W + 2 * wo + (k & 1);
       float v[VE];
       Pack16<T>::load(x + (size_t)pin * x_ld + x_off + c0, v);
+      if (sc) {  // folded BN: pool y = r*s + h (the max of y, whatever the sign of s)
+#pragma unroll
+        for (int e = 0; e < VE; ++e) v[e] = v[e] * sc[c0 + e] + sh[c0 + e];
+      }
 #pragma unroll
       for (int e = 0; e < VE; ++e) {
         if (k == 0 || v[e] > best[e]) {
@@ -482,16 +507,17 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
 }
 
 extern "C" int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h,
-                                      int w, int c, void* y, uint8_t* idx, void* stream) {
+                                      int w, int c, void* y, uint8_t* idx, const float* scale,
+                                      const float* shift, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   CNN_REQUIRE(c % 8 == 0 && x_ld % 8 == 0 && x_off % 8 == 0, "maxpool_fwd: channels must be multiples of 8");
   const long work = (long)n * (h / 2) * (w / 2) * c;
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(grid_for(work / 8)), dim3(256), 0, s,
-                       (const bf16*)x, (long)x_ld, x_off, n, h, w, c, (bf16*)y, idx);
+                       (const bf16*)x, (long)x_ld, x_off, n, h, w, c, (bf16*)y, idx, scale, shift);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid_for(work / 4)), dim3(256), 0, s,
-                       (const float*)x, (long)x_ld, x_off, n, h, w, c, (float*)y, idx);
+                       (const float*)x, (long)x_ld, x_off, n, h, w, c, (float*)y, idx, scale, shift);
   return cnnitmo_check_launch("maxpool_fwd");
 }
 
@@ -523,18 +549,27 @@ template <typename T, bool BWD>
 __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W, int cin,
                             const float* __restrict__ wt, const float* __restrict__ bias,
                             const float* __restrict__ target, float* __restrict__ yhat,
-                            T* __restrict__ dx, float inv_numel, float* __restrict__ part) {
+                            T* __restrict__ dx, float inv_numel, float* __restrict__ part,
+                            const float* __restrict__ fs, const float* __restrict__ fh) {
   constexpr int VE = Vec16<T>::N;
   const int lpp = cin / VE;             // lanes per pixel (power of two <= 64)
   const int ppb = 256 / lpp;            // pixels per block iteration
   const int tid = threadIdx.x, sub = tid % lpp, slot = tid / lpp;
   const int c0 = sub * VE;
-  float w[3][VE];
+  float w[3][VE], wf[3][VE];  // raw (for dx) and BN-folded (for z) weights
+  float bfold[3] = {0.f, 0.f, 0.f};
 #pragma unroll
   for (int o = 0; o < 3; ++o)
 #pragma unroll
-    for (int e = 0; e < VE; ++e) w[o][e] = wt[o * cin + c0 + e];
-  const float b0 = bias[0], b1 = bias[1], b2 = bias[2];
+    for (int e = 0; e < VE; ++e) {
+      w[o][e] = wt[o * cin + c0 + e];
+      wf[o][e] = fs ? w[o][e] * fs[c0 + e] : w[o][e];
+      if (fh) bfold[o] += w[o][e] * fh[c0 + e];
+    }
+#pragma unroll
+  for (int o = 0; o < 3; ++o)
+    for (int off = lpp >> 1; off > 0; off >>= 1) bfold[o] += __shfl_xor(bfold[o], off, 64);
+  const float b0 = bias[0] + bfold[0], b1 = bias[1] + bfold[1], b2 = bias[2] + bfold[2];
   float dwacc[3][VE];
 #pragma unroll
   for (int o = 0; o < 3; ++o)
@@ -555,7 +590,7 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
     for (int o = 0; o < 3; ++o) {
       float s = 0.f;
 #pragma unroll
-      for (int e = 0; e < VE; ++e) s += v[e] * w[o][e];
+      for (int e = 0; e < VE; ++e) s += v[e] * wf[o][e];
       for (int off = lpp >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
       z[o] = s;
     }
@@ -631,7 +666,8 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
 }
 
 extern "C" int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
-                                const float* wt, const float* b, float* yhat, void* stream) {
+                                const float* wt, const float* b, const float* scale,
+                                const float* shift, float* yhat, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
   CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
@@ -640,16 +676,17 @@ extern "C" int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_va
   const int G = cnnitmo_head_rows(P);
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL((head_kernel<bf16, false>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
-                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr);
+                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale, shift);
   else
     hipLaunchKernelGGL((head_kernel<float, false>), dim3(G), dim3(256), 0, s, (const float*)x, n, h,
-                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr);
+                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale, shift);
   return cnnitmo_check_launch("head_fwd");
 }
 
 extern "C" int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w,
-                                    int cin, const float* wt, const float* b, const float* target,
-                                    void* dx, float* part, void* stream) {
+                                    int cin, const float* wt, const float* b, const float* scale,
+                                    const float* shift, const float* target, void* dx, float* part,
+                                    void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
   CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
@@ -659,34 +696,41 @@ extern "C" int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int 
   const float inv_numel = (float)(1.0 / ((double)n * h_valid * w * 3));
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL((head_kernel<bf16, true>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
-                       h_valid, w, cin, wt, b, target, nullptr, (bf16*)dx, inv_numel, part);
+                       h_valid, w, cin, wt, b, target, nullptr, (bf16*)dx, inv_numel, part, scale, shift);
   else
     hipLaunchKernelGGL((head_kernel<float, true>), dim3(G), dim3(256), 0, s, (const float*)x, n, h,
-                       h_valid, w, cin, wt, b, target, nullptr, (float*)dx, inv_numel, part);
+                       h_valid, w, cin, wt, b, target, nullptr, (float*)dx, inv_numel, part, scale, shift);
   return cnnitmo_check_launch("head_fwd_bwd");
 }
 
+// Folded input BN (x = r, y = r*s + h): dW[o][c] = s[c]*sum(dz*r) + h[c]*db[o].
 __global__ void head_final_kernel(const double* __restrict__ ws, int G, int cin, double numel,
-                                  float* loss_acc, float* dw, float* db) {
+                                  float* loss_acc, float* dw, float* db, const float* fs,
+                                  const float* fh) {
   const int ncol = 5 + 3 * cin;
   const int k = wave_col();
   if (k < ncol) {
     const double s = fold(ws, G, ncol, k);
+    double dbo = 0.0;
+    if (k >= 5 && fh) dbo = fold(ws, G, ncol, 2 + (k - 5) / cin);
     if ((threadIdx.x & 63) != 0) return;
     if (k == 0) loss_acc[0] = (float)(s / numel);
     else if (k == 1) loss_acc[1] = (float)(s / (numel / 3.0));
     else if (k < 5) db[k - 2] = (float)s;
-    else dw[k - 5] = (float)s;
+    else {
+      const int c = (k - 5) % cin;
+      dw[k - 5] = (float)((fs ? s * fs[c] : s) + (fh ? dbo * fh[c] : 0.0));
+    }
   }
 }
 
 extern "C" int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
-                                     float* loss_acc, float* dw, float* db, void* workspace,
-                                     void* stream) {
+                                     const float* scale, const float* shift, float* loss_acc,
+                                     float* dw, float* db, void* workspace, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int G = colsum_stage1_launch(part, rows, 5 + 3 * cin, workspace, s);
   hipLaunchKernelGGL(head_final_kernel, dim3(wave_grid(5 + 3 * cin)), dim3(256), 0, s, (const double*)workspace, G, cin,
-                     numel, loss_acc, dw, db);
+                     numel, loss_acc, dw, db, scale, shift);
   return cnnitmo_check_launch("head_finalize");
 }
 
@@ -857,4 +901,156 @@ extern "C" int cnnitmo_im2col_c3(int dtype, const float* x, int n, int h_valid, 
     hipLaunchKernelGGL(im2col_c3_kernel<float>, dim3(grid_for(work * 2)), dim3(256), 0, s, x, n,
                        h_valid, h, w, (float*)cols);
   return cnnitmo_check_launch("im2col_c3");
+}
+
+// ----------------------------------------------------------------------------
+// BN folding (training): a consumer of a BN output y = r*s + h (per input
+// channel) reads the stored r and folds the affine instead of materialising y.
+//   conv3x3: W' = W*s, bias' = b + sum_t u_t, u_t[co] = sum_ci W[co][t][ci] h[ci];
+//            zero padding applies to y, so the conv epilogue subtracts u_t for every
+//            out-of-bounds tap t of a border pixel via the table
+//            border[co] = {Utop, Ubot, Uleft, Uright, u0, u2, u6, u8}.
+//   tconv:   K' = K*s, bias'[tap][co] = b[co] + sum_ci K[tap][co][ci] h[ci] (no padding).
+// ----------------------------------------------------------------------------
+__device__ float block_sum_det(float v, float* red) {
+  // deterministic 256-thread tree sum; every thread returns the total
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  const float s = red[0];
+  __syncthreads();
+  return s;
+}
+
+template <typename T>
+__global__ void fold_conv_kernel(const float* __restrict__ w, const float* __restrict__ b,
+                                 const float* __restrict__ s, const float* __restrict__ h, int cout,
+                                 int cin, int ntaps, T* __restrict__ wout, float* __restrict__ bout,
+                                 float* __restrict__ border) {
+  __shared__ float red[256];
+  const int co = blockIdx.x;
+  float u[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {  // ntaps == 9
+    float acc = 0.f;
+    for (int ci = threadIdx.x; ci < cin; ci += blockDim.x) {
+      const size_t i = ((size_t)co * ntaps + t) * cin + ci;
+      const float wv = w[i];
+      wout[i] = from_f32<T>(s ? wv * s[ci] : wv);
+      if (h) acc += wv * h[ci];
+    }
+    u[t] = block_sum_det(acc, red);
+  }
+  if (threadIdx.x == 0) {
+    float bsum = b ? b[co] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) bsum += u[t];
+    bout[co] = bsum;
+    if (border && ntaps == 9) {
+      float* U = border + (size_t)co * 8;
+      U[0] = u[0] + u[1] + u[2];
+      U[1] = u[6] + u[7] + u[8];
+      U[2] = u[0] + u[3] + u[6];
+      U[3] = u[2] + u[5] + u[8];
+      U[4] = u[0];
+      U[5] = u[2];
+      U[6] = u[6];
+      U[7] = u[8];
+    }
+  }
+}
+
+extern "C" int cnnitmo_fold_conv3x3(int dtype, const float* w, const float* bias, const float* scale,
+                                    const float* shift, int cout, int cin, void* w_out,
+                                    float* bias_out, float* border, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(fold_conv_kernel<bf16>, dim3(cout), dim3(256), 0, s, w, bias, scale, shift, cout,
+                       cin, 9, (bf16*)w_out, bias_out, border);
+  else
+    hipLaunchKernelGGL(fold_conv_kernel<float>, dim3(cout), dim3(256), 0, s, w, bias, scale, shift,
+                       cout, cin, 9, (float*)w_out, bias_out, border);
+  return cnnitmo_check_launch("fold_conv3x3");
+}
+
+// tconv: k [4][cout][cin] viewed as [4*cout rows][cin]: one block per (tap, co)
+template <typename T>
+__global__ void fold_tconv_kernel(const float* __restrict__ k, const float* __restrict__ b,
+                                  const float* __restrict__ s, const float* __restrict__ h, int cout,
+                                  int cin, T* __restrict__ kout, float* __restrict__ bout) {
+  __shared__ float red[256];
+  const int row = blockIdx.x, co = row % cout;
+  float acc = 0.f;
+  for (int ci = threadIdx.x; ci < cin; ci += blockDim.x) {
+    const size_t i = (size_t)row * cin + ci;
+    const float kv = k[i];
+    kout[i] = from_f32<T>(s ? kv * s[ci] : kv);
+    if (h) acc += kv * h[ci];
+  }
+  const float tot = block_sum_det(acc, red);
+  if (threadIdx.x == 0) bout[row] = (b ? b[co] : 0.f) + tot;
+}
+
+extern "C" int cnnitmo_fold_tconv2x2(int dtype, const float* k, const float* bias, const float* scale,
+                                     const float* shift, int cout, int cin, void* k_out,
+                                     float* bias_out, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(fold_tconv_kernel<bf16>, dim3(4 * cout), dim3(256), 0, s, k, bias, scale, shift,
+                       cout, cin, (bf16*)k_out, bias_out);
+  else
+    hipLaunchKernelGGL(fold_tconv_kernel<float>, dim3(4 * cout), dim3(256), 0, s, k, bias, scale, shift,
+                       cout, cin, (float*)k_out, bias_out);
+  return cnnitmo_check_launch("fold_tconv2x2");
+}
+
+// Border sums of an output gradient dz [n][h][w][c] for the folded-BN conv
+// weight-gradient correction: rows [n*BS_SEG][8][c] of partials (reduce with
+// cnnitmo_colsum) = {row 0, row h-1, col 0, col w-1, (0,0), (0,w-1), (h-1,0), (h-1,w-1)}.
+constexpr int BS_SEG = 16;
+template <typename T>
+__global__ void border_sums_kernel(const T* __restrict__ dz, int H, int W, int C,
+                                   float* __restrict__ part) {
+  const int img = blockIdx.x / BS_SEG, seg = blockIdx.x % BS_SEG;
+  const T* base = dz + (size_t)img * H * W * C;
+  float* out = part + (size_t)blockIdx.x * 8 * C;
+  const int w0 = (int)((long)W * seg / BS_SEG), w1 = (int)((long)W * (seg + 1) / BS_SEG);
+  const int h0 = (int)((long)H * seg / BS_SEG), h1 = (int)((long)H * (seg + 1) / BS_SEG);
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float top = 0.f, bot = 0.f, lef = 0.f, rig = 0.f;
+    for (int w = w0; w < w1; ++w) {
+      top += to_f32(base[(size_t)w * C + c]);
+      bot += to_f32(base[((size_t)(H - 1) * W + w) * C + c]);
+    }
+    for (int hh = h0; hh < h1; ++hh) {
+      lef += to_f32(base[((size_t)hh * W) * C + c]);
+      rig += to_f32(base[((size_t)hh * W + W - 1) * C + c]);
+    }
+    const bool s0 = seg == 0;
+    out[0 * C + c] = top;
+    out[1 * C + c] = bot;
+    out[2 * C + c] = lef;
+    out[3 * C + c] = rig;
+    out[4 * C + c] = s0 ? to_f32(base[c]) : 0.f;
+    out[5 * C + c] = s0 ? to_f32(base[(size_t)(W - 1) * C + c]) : 0.f;
+    out[6 * C + c] = s0 ? to_f32(base[((size_t)(H - 1) * W) * C + c]) : 0.f;
+    out[7 * C + c] = s0 ? to_f32(base[((size_t)(H - 1) * W + W - 1) * C + c]) : 0.f;
+  }
+}
+
+extern "C" int cnnitmo_border_rows(int n) { return n * BS_SEG; }
+
+extern "C" int cnnitmo_border_sums(int dtype, const void* dz, int n, int h, int w, int c, float* part,
+                                   void* stream) {
+  CNN_REQUIRE(n > 0 && h > 0 && w > 0 && c > 0, "border_sums: empty");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(border_sums_kernel<bf16>, dim3(n * BS_SEG), dim3(256), 0, s, (const bf16*)dz, h, w, c, part);
+  else
+    hipLaunchKernelGGL(border_sums_kernel<float>, dim3(n * BS_SEG), dim3(256), 0, s, (const float*)dz, h, w, c, part);
+  return cnnitmo_check_launch("border_sums");
 }

@@ -1,0 +1,93 @@
+// Shared declarations of the forward-family implicit-GEMM kernels.
+#pragma once
+#include "common.h"
+
+struct FwdArgs {
+  const void* a;
+  long a_ld;
+  int a_off;
+  int nimg, hs, ws;  // source grid
+  int ho, wo;        // iteration grid (GEMM rows are its pixels)
+  int scale;         // source pixel = (h*scale + dy[t], w*scale + dx[t])
+  int ntaps;
+  int dyc, dxc;  // tap t offset = ((code >> 2t) & 3) - 1 (2-bit fields, no dynamic indexing)
+  int cin;  // channels per tap
+  const void* b;
+  int N;
+  long M;
+  const float* bias;
+  void* out;
+  long out_ld;
+  int out_off;
+  int scatter;  // tconv 2x2 s2 scatter: column n = tap*cout + co
+  int cout;
+  int flags;
+  const float* aff_scale;
+  const float* aff_shift;
+  float* stats;  // [mblocks][2][N]
+  int mblocks, nblocks;
+  const float* border;  // folded-BN zero-padding correction [cout][8] (conv3x3 fwd), or null
+};
+
+// Out-of-bounds-tap correction for a folded BN shift (see cnnitmo_fold_conv3x3):
+// pixel (oh, ow) of an ho x wo 'same' conv loses sum_{t OOB} u_t[co].
+__device__ __forceinline__ float border_corr(const float* __restrict__ U, int oh, int ow, int ho, int wo) {
+  const bool top = oh == 0, bot = oh == ho - 1, lef = ow == 0, rig = ow == wo - 1;
+  if (!(top | bot | lef | rig)) return 0.f;
+  float c = 0.f;
+  if (top) c += U[0];
+  if (bot) c += U[1];
+  if (lef) c += U[2];
+  if (rig) c += U[3];
+  if (top & lef) c -= U[4];
+  if (top & rig) c -= U[5];
+  if (bot & lef) c -= U[6];
+  if (bot & rig) c -= U[7];
+  return c;
+}
+
+template <typename T> struct Mma;
+template <> struct Mma<bf16> {
+  static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                 __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  }
+};
+template <> struct Mma<float> {
+  static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+  }
+};
+
+
+// v2 (direct-to-LDS pipelined) forward family, igemm_fwd2.hip
+template <typename T>
+int launch_fwd2(FwdArgs a, hipStream_t s, const char* what);
+int fwd2_stat_rows(long m);
+bool fwd2_handles(int N);  // v2 is the faster kernel for this column count
+
+// v2 (direct-to-LDS, multi-tap) bf16 weight gradients, igemm_wgrad2.hip
+struct Wgrad2Args {
+  const bf16* a;  // A operand source (gradient): channels m
+  long a_ld;
+  int a_off, ha, wa, a_scale;
+  const bf16* b;  // B operand source (activation): channels n
+  long b_ld;
+  int b_off, hb, wb, b_scale;
+  int nimg, hg, wg;
+  int ntaps;
+  int ayc, axc, byc, bxc;  // per-tap offsets (2-bit fields, value+1)
+  int a_tapdep;            // 1: A depends on the tap (tconv), 0: B does (conv)
+  int M, N;
+  float* out;
+  long split_stride, tap_stride;
+  int out_ld;
+  int mblocks, nblocks, tgroups, splits;
+  long P, pix_per_split;
+};
+
+int launch_wgrad2(Wgrad2Args a, void* ws, size_t ws_bytes, hipStream_t s);
+size_t wgrad2_ws_bytes(long P, int M, int N, int ntaps);

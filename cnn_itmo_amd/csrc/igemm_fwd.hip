@@ -18,51 +18,10 @@
 // group g owns channels 4g..4g+3 so each lane reads one 16-byte fragment per
 // 4 MFMAs).  Epilogue: bias, ReLU, optional inference BN affine, BN partial
 // sums (deterministic per-tile slabs), store (plain or tconv pixel-scatter).
+#include <cstdlib>
 #include <cstring>
 
-#include "common.h"
-
-struct FwdArgs {
-  const void* a;
-  long a_ld;
-  int a_off;
-  int nimg, hs, ws;  // source grid
-  int ho, wo;        // iteration grid (GEMM rows are its pixels)
-  int scale;         // source pixel = (h*scale + dy[t], w*scale + dx[t])
-  int ntaps;
-  int dyc, dxc;  // tap t offset = ((code >> 2t) & 3) - 1 (2-bit fields, no dynamic indexing)
-  int cin;  // channels per tap
-  const void* b;
-  int N;
-  long M;
-  const float* bias;
-  void* out;
-  long out_ld;
-  int out_off;
-  int scatter;  // tconv 2x2 s2 scatter: column n = tap*cout + co
-  int cout;
-  int flags;
-  const float* aff_scale;
-  const float* aff_shift;
-  float* stats;  // [mblocks][2][N]
-  int mblocks, nblocks;
-};
-
-template <typename T> struct Mma;
-template <> struct Mma<bf16> {
-  static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                 __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
-  }
-};
-template <> struct Mma<float> {
-  static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-  }
-};
+#include "igemm_common.h"
 
 // LDS image of a [rows][64 B] tile: 16-byte chunk c of row r stored at slot
 // c ^ (((r >> 3) & 1) << 1).  With 16-row MFMA groups read by ds_read_b128
@@ -210,7 +169,7 @@ __global__ __launch_bounds__(256) void igemm_fwd_kernel(const FwdArgs p) {
     }
     coj[j] = co;
     tapoff[j] = (tp >> 1) * 2 * p.wo + (tp & 1);
-    bj[j] = p.bias ? p.bias[co] : 0.f;
+    bj[j] = p.bias ? p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : co] : 0.f;
     sj[j] = aff ? p.aff_scale[co] : 1.f;
     hj[j] = aff ? p.aff_shift[co] : 0.f;
   }
@@ -224,6 +183,12 @@ __global__ __launch_bounds__(256) void igemm_fwd_kernel(const FwdArgs p) {
     for (int r = 0; r < 4; ++r) {
       const long m = m0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
       if (m >= p.M) continue;
+      int boh = 1, bow = 1;
+      if (p.border) {
+        const int rem = (int)(m % hw);
+        boh = rem / p.wo;
+        bow = rem - boh * p.wo;
+      }
       long pixbase;
       if (p.scatter) {
         const int img = (int)(m / hw);
@@ -236,6 +201,7 @@ __global__ __launch_bounds__(256) void igemm_fwd_kernel(const FwdArgs p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         float v = acc[i][j][r] + bj[j];
+        if (p.border) v -= border_corr(p.border + (size_t)coj[j] * 8, boh, bow, p.ho, p.wo);
         if (relu) v = fmaxf(v, 0.f);
         if (aff) v = v * sj[j] + hj[j];
         s1[j] += v;
@@ -316,8 +282,20 @@ int launch_fwd(FwdArgs a, hipStream_t s, const char* what) {
   return cnnitmo_check_launch(what);
 }
 
+bool use_v1() {
+  static const bool v1 = [] {
+    const char* e = getenv("CNNITMO_FWD_V1");
+    return e && atoi(e) == 1;
+  }();
+  return v1;
+}
+
 int dispatch(int dtype, const FwdArgs& a, void* stream, const char* what) {
   hipStream_t s = (hipStream_t)stream;
+  if (!use_v1() && fwd2_handles(a.N)) {
+    if (dtype == CNNITMO_BF16) return launch_fwd2<bf16>(a, s, what);
+    if (dtype == CNNITMO_F32) return launch_fwd2<float>(a, s, what);
+  }
   if (dtype == CNNITMO_BF16) return launch_fwd<bf16>(a, s, what);
   if (dtype == CNNITMO_F32) return launch_fwd<float>(a, s, what);
   cnnitmo_set_error("%s: unsupported dtype %d", what, dtype);
@@ -347,6 +325,7 @@ void set_taps3x3(FwdArgs& a) {
 
 extern "C" int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols) {
   (void)dtype;
+  if (!use_v1() && fwd2_handles(ncols)) return fwd2_stat_rows(m);
   Cfg c = pick_cfg(ncols);
   return (int)((m + c.bm - 1) / c.bm);
 }
@@ -355,7 +334,7 @@ extern "C" int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off
                                    int w, int cin, const void* wt, const float* bias, int cout,
                                    void* out, int out_ld, int out_off, int flags,
                                    const float* aff_scale, const float* aff_shift,
-                                   float* stat_part, void* stream) {
+                                   float* stat_part, const float* border, void* stream) {
   FwdArgs a = base_args();
   a.a = x; a.a_ld = x_ld; a.a_off = x_off;
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
@@ -364,6 +343,7 @@ extern "C" int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off
   a.bias = bias; a.out = out; a.out_ld = out_ld; a.out_off = out_off;
   a.cout = cout; a.flags = flags; a.aff_scale = aff_scale; a.aff_shift = aff_shift;
   a.stats = stat_part;
+  a.border = border;
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || stat_part, "conv3x3_fwd: STATS without buffer");
   CNN_REQUIRE(!(flags & CNNITMO_AFFINE) || (aff_scale && aff_shift), "conv3x3_fwd: AFFINE without coefficients");
   return dispatch(dtype, a, stream, "conv3x3_fwd");

@@ -1,0 +1,354 @@
+// Implicit-GEMM convolution, forward family, v2: direct-to-LDS pipelined MFMA.
+//
+// Same GEMM as igemm_fwd.hip (C[m][n] = sum_k A[m][k] B[n][k], m = output pixel,
+// k = (tap, channel), A gathered per tap from an NHWC source with zero
+// padding), restructured for gfx950's memory pipeline:
+//   * operands go HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR staging):
+//     each lane supplies its own gather address (padding rows point at a zero
+//     page); the LDS image is lane-linear, so the XOR swizzle is applied to the
+//     SOURCE chunk and mirrored on the ds_read (guide rule 21);
+//   * K-step = 128 bytes per row (64 bf16 / 32 f32), flat over (tap, channel)
+//     so Cin = 32 or 96 and tap-straddling steps need no special case;
+//   * ST-stage LDS ring with counted `s_waitcnt vmcnt` and ONE raw s_barrier per
+//     K-step: loads for steps t+1..t+ST-1 stay in flight across the barrier
+//     while step t is multiplied;
+//   * epilogue (bias, ReLU, inference BN affine, BN partial sums) in registers,
+//     then the tile is staged through LDS and stored as 16-byte row vectors
+//     (plain NHWC view or the Conv2DTranspose pixel scatter).
+// LDS image: [rows][128 B], 16-byte chunk c of row r at slot c ^ ((r >> 1) & 7):
+// conflict-free for the fragment reads (lane l: row l&15, chunk 4*kk + (l>>4))
+// in every ds_read_b128 bank group (derivation in DESIGN.md).
+#include <cstdlib>
+
+#include "igemm_common.h"
+
+__device__ __attribute__((aligned(256))) unsigned char g_zero_page[256] = {0};
+
+// One LDS-DMA wave-instruction: lane l copies 16 bytes from its own gsrc to
+// LDS[lds + 16*l].  Issued from inline asm on purpose: when hipcc sees the
+// builtin it cannot prove later ds_reads of OTHER ring slots don't alias the
+// in-flight DMA and inserts s_waitcnt vmcnt(0) before them, serialising the
+// pipeline.  Ordering is instead guaranteed by the counted vmcnt + s_barrier
+// protocol of the main loop (and the "memory" clobber).
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void glds16(const void* gsrc, const char* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(a) : "m0");
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int swz_off(int row, int chunk) {
+  return (row << 7) + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int ST>
+struct Fwd2Cfg {
+  static constexpr int NW = WM * WN, NT = NW * 64;
+  static constexpr int VE = Vec16<T>::N, KE = 8 * VE;
+  static constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  static constexpr int A_INSTR = BM / 8, B_INSTR = BN / 8;
+  static constexpr int NA = A_INSTR / NW, NB = B_INSTR / NW;
+  static constexpr int L = NA + NB;  // glds per wave per stage
+  static constexpr int STAGE = (BM + BN) * 128;
+  static constexpr int CLD = BN + 16 / (int)sizeof(T);  // padded C-tile row (elements)
+  static constexpr int C_BYTES = BM * CLD * (int)sizeof(T);
+  static constexpr int SMEM = (ST * STAGE > C_BYTES + WM * BN * 8) ? ST * STAGE : C_BYTES + WM * BN * 8;
+  static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "loads must split evenly over waves");
+  static_assert(NA % 2 == 0, "A row-block parity must be compile-time");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+template <typename T, int BM, int BN, int WM, int WN, int ST>
+__global__ __launch_bounds__(WM * WN * 64) void igemm_fwd2_kernel(const FwdArgs p) {
+  using C = Fwd2Cfg<T, BM, BN, WM, WN, ST>;
+  constexpr int VE = C::VE, KE = C::KE, TM = C::TM, TN = C::TN, FM = C::FM, FN = C::FN;
+  constexpr int NA = C::NA, NB = C::NB, STAGE = C::STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int lid = xcd_remap(blockIdx.x, p.mblocks * p.nblocks);
+  const int mb = lid / p.nblocks, nb = lid - mb * p.nblocks;
+  const long m0 = (long)mb * BM;
+  const int n0 = nb * BN;
+  const int K = p.ntaps * p.cin;
+  const int nk = (K + KE - 1) / KE;
+  const T* __restrict__ A = (const T*)p.a;
+  const T* __restrict__ B = (const T*)p.b;
+
+  // ---- per-lane load bookkeeping -------------------------------------------
+  const int sub = lane >> 3, pslot = lane & 7;
+  // logical chunk held by this lane's LDS slot: pslot ^ ((row >> 1) & 7), row = blk*8 + sub
+  const int cA0 = pslot ^ (sub >> 1), cA1 = cA0 ^ 4;  // row block even / odd
+  int a_img[NA], a_h[NA], a_w[NA];
+  const long hw = (long)p.ho * p.wo;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const long m = m0 + (wave * NA + i) * 8 + sub;
+    a_img[i] = -1;
+    a_h[i] = a_w[i] = 0;
+    if (m < p.M) {
+      const int img = (int)(m / hw);
+      const int rem = (int)(m - (long)img * hw);
+      const int oh = rem / p.wo;
+      a_img[i] = img;
+      a_h[i] = oh * p.scale;
+      a_w[i] = (rem - oh * p.wo) * p.scale;
+    }
+  }
+  // (tap, channel) of the chunk this lane loads, for even/odd row blocks
+  int tap0 = (cA0 * VE) / p.cin, ch0 = (cA0 * VE) - tap0 * p.cin;
+  int tap1 = (cA1 * VE) / p.cin, ch1 = (cA1 * VE) - tap1 * p.cin;
+  int kb0 = cA0 * VE, kb1 = cA1 * VE;  // B-side k of the same chunks
+
+  auto advance = [&]() {
+    ch0 += KE;
+    while (ch0 >= p.cin) { ch0 -= p.cin; ++tap0; }
+    ch1 += KE;
+    while (ch1 >= p.cin) { ch1 -= p.cin; ++tap1; }
+    kb0 += KE;
+    kb1 += KE;
+  };
+
+  auto issue = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + BM * 128;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int tap = (i & 1) ? tap1 : tap0;
+      const int ch = (i & 1) ? ch1 : ch0;
+      const void* src = g_zero_page;
+      if (a_img[i] >= 0 && tap < p.ntaps) {
+        const int hh = a_h[i] + ((p.dyc >> (2 * tap)) & 3) - 1;
+        const int ww = a_w[i] + ((p.dxc >> (2 * tap)) & 3) - 1;
+        if ((unsigned)hh < (unsigned)p.hs && (unsigned)ww < (unsigned)p.ws)
+          src = A + ((size_t)((long)a_img[i] * p.hs + hh) * p.ws + ww) * p.a_ld + p.a_off + ch;
+      }
+      glds16(src, As + (wave * NA + i) * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int blk = wave * NB + i;
+      const int k = (blk & 1) ? kb1 : kb0;
+      const void* src = g_zero_page;
+      if (k < K) src = B + (size_t)(n0 + blk * 8 + sub) * K + k;
+      glds16(src, Bs + blk * 1024);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 128;
+    const int frow = lane & 15, fg = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      uint4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const uint4*>(As + swz_off(wm * TM + i * 16 + frow, kk * 4 + fg));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const uint4*>(Bs + swz_off(wn * TN + j * 16 + frow, kk * 4 + fg));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) Mma<T>::run(acc[i][j], af[i], bfr[j]);
+    }
+  };
+
+  // ---- main loop: ST-stage ring, one barrier per K-step ----------------------
+  issue(0);
+  advance();
+#pragma unroll
+  for (int s = 1; s < ST - 1; ++s)
+    if (s < nk) { issue(s); advance(); }
+  for (int t = 0; t < nk; ++t) {
+    if constexpr (ST == 3) {
+      if (t + 1 < nk) wait_vm<C::L>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // compiler fence: no LDS read hoisted above the barrier
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + ST - 1 < nk) {
+      issue((t + ST - 1) % ST);
+      advance();
+    }
+    compute(t % ST);
+  }
+  __syncthreads();
+
+  // ---- epilogue ----------------------------------------------------------------
+  const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE,
+             stats = p.flags & CNNITMO_STATS;
+  float bj[FN], sj[FN], hj[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * TN + j * 16 + (lane & 15);
+    const int co = p.scatter ? n % p.cout : n;
+    bj[j] = p.bias ? p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : co] : 0.f;
+    sj[j] = aff ? p.aff_scale[co] : 1.f;
+    hj[j] = aff ? p.aff_shift[co] : 0.f;
+  }
+  float s1[FN], s2[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) s1[j] = s2[j] = 0.f;
+  T* Cs = reinterpret_cast<T*>(smem);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+      const bool valid = m0 + row < p.M;
+      int boh = 1, bow = 1;  // interior unless a border table is given
+      if (p.border && valid) {
+        const long m = m0 + row;
+        const int rem = (int)(m % hw);
+        boh = rem / p.wo;
+        bow = rem - boh * p.wo;
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float v = acc[i][j][r] + bj[j];
+        if (p.border)
+          v -= border_corr(p.border + (size_t)(n0 + wn * TN + j * 16 + (lane & 15)) * 8, boh, bow, p.ho, p.wo);
+        if (relu) v = fmaxf(v, 0.f);
+        if (aff) v = v * sj[j] + hj[j];
+        if (valid) {
+          s1[j] += v;
+          s2[j] += v * v;
+        }
+        Cs[row * C::CLD + wn * TN + j * 16 + (lane & 15)] = from_f32<T>(v);
+      }
+    }
+  if (stats) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      s1[j] += __shfl_xor(s1[j], 16, 64);
+      s1[j] += __shfl_xor(s1[j], 32, 64);
+      s2[j] += __shfl_xor(s2[j], 16, 64);
+      s2[j] += __shfl_xor(s2[j], 32, 64);
+    }
+    float* red = reinterpret_cast<float*>(smem + C::C_BYTES);  // [WM][BN][2]
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = wn * TN + j * 16 + lane;
+        red[(wm * BN + col) * 2 + 0] = s1[j];
+        red[(wm * BN + col) * 2 + 1] = s2[j];
+      }
+    }
+  }
+  __syncthreads();
+  if (stats && tid < BN) {
+    const float* red = reinterpret_cast<const float*>(smem + C::C_BYTES);
+    float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) {
+      t1 += red[(w * BN + tid) * 2 + 0];
+      t2 += red[(w * BN + tid) * 2 + 1];
+    }
+    float* st = p.stats + (size_t)mb * 2 * p.N;
+    st[n0 + tid] = t1;
+    st[p.N + n0 + tid] = t2;
+  }
+  // coalesced 16-byte row stores
+  T* __restrict__ O = (T*)p.out;
+  constexpr int CPR = BN / VE;  // chunks per row
+  for (int idx = tid; idx < BM * CPR; idx += C::NT) {
+    const int row = idx / CPR, cc = idx - row * CPR;
+    const long m = m0 + row;
+    if (m >= p.M) continue;
+    const uint4 v = *reinterpret_cast<const uint4*>(Cs + row * C::CLD + cc * VE);
+    const int n = n0 + cc * VE;
+    size_t off;
+    if (p.scatter) {
+      const int tp = n / p.cout, co = n - tp * p.cout;
+      const int img = (int)(m / hw);
+      const int rem = (int)(m - (long)img * hw);
+      const int ii = rem / p.wo, jj = rem - ii * p.wo;
+      const long pix = ((long)img * 2 * p.ho + 2 * ii + (tp >> 1)) * 2 * p.wo + 2 * jj + (tp & 1);
+      off = (size_t)pix * p.out_ld + p.out_off + co;
+    } else {
+      off = (size_t)m * p.out_ld + p.out_off + n;
+    }
+    *reinterpret_cast<uint4*>(O + off) = v;
+  }
+}
+
+// ----------------------------------------------------------------------------
+namespace {
+struct Cfg2 {
+  int bn;
+};
+// Tile choice (measured on MI355X, tools/bench_layers.py): the 8-wave 256x128
+// tile with a 3-deep ring for N % 128 == 0; otherwise 4-wave 256-row tiles with a
+// 2-deep ring (2 blocks/CU hide the gather latency better than a deeper ring at
+// 1 block/CU).  N == 32 stays on v1 (see use_fwd2()).
+Cfg2 pick2(int N) {
+  if (N % 128 == 0) return {128};
+  if (N % 64 == 0) return {64};
+  if (N % 96 == 0) return {96};
+  return {32};
+}
+
+int stages_for(int bn) {
+  static const int env = [] {
+    const char* e = getenv("CNNITMO_STAGES");
+    return e ? atoi(e) : 0;
+  }();
+  if (env == 2 || env == 3) return env;
+  return bn == 128 ? 3 : 2;
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+void launch_st(const FwdArgs& a, hipStream_t s, dim3 grid) {
+  if (stages_for(BN) == 2)
+    hipLaunchKernelGGL((igemm_fwd2_kernel<T, BM, BN, WM, WN, 2>), grid, dim3(WM * WN * 64), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_fwd2_kernel<T, BM, BN, WM, WN, 3>), grid, dim3(WM * WN * 64), 0, s, a);
+}
+}  // namespace
+
+int fwd2_stat_rows(long m) { return (int)((m + 255) / 256); }
+bool fwd2_handles(int N) { return N != 32; }
+
+template <typename T>
+int launch_fwd2(FwdArgs a, hipStream_t s, const char* what) {
+  constexpr int VE = Vec16<T>::N;
+  CNN_REQUIRE(a.N % 32 == 0, "%s: output columns %d not a multiple of 32", what, a.N);
+  CNN_REQUIRE(a.cin % VE == 0, "%s: channels per tap %d not a multiple of %d", what, a.cin, VE);
+  CNN_REQUIRE(a.a_ld % VE == 0 && a.a_off % VE == 0 && a.out_ld % VE == 0 && a.out_off % VE == 0,
+              "%s: views must be 16-byte aligned", what);
+  CNN_REQUIRE(!a.scatter || a.cout % VE == 0, "%s: scatter needs cout %% %d == 0", what, VE);
+  CNN_REQUIRE(a.M > 0 && a.ntaps >= 1 && a.ntaps <= 9, "%s: bad sizes", what);
+  const Cfg2 c = pick2(a.N);
+  a.mblocks = (int)((a.M + 255) / 256);
+  a.nblocks = a.N / c.bn;
+  const long total = (long)a.mblocks * a.nblocks;
+  CNN_REQUIRE(total < (1L << 31), "%s: grid too large", what);
+  const dim3 grid((unsigned)total);
+  switch (c.bn) {
+    case 128: launch_st<T, 256, 128, 4, 2>(a, s, grid); break;
+    case 96: launch_st<T, 256, 96, 4, 1>(a, s, grid); break;
+    case 64: launch_st<T, 256, 64, 4, 1>(a, s, grid); break;
+    default: launch_st<T, 256, 32, 4, 1>(a, s, grid); break;
+  }
+  return cnnitmo_check_launch(what);
+}
+
+template int launch_fwd2<bf16>(FwdArgs, hipStream_t, const char*);
+template int launch_fwd2<float>(FwdArgs, hipStream_t, const char*);

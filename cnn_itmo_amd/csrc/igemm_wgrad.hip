@@ -17,7 +17,9 @@
 #include <algorithm>
 #include <cstring>
 
-#include "common.h"
+#include <cstdlib>
+
+#include "igemm_common.h"
 
 struct WgradArgs {
   const void* a;
@@ -264,9 +266,42 @@ __global__ __launch_bounds__(256) void igemm_wgrad_kernel(const WgradArgs p) {
     }
 }
 
-// Sum the split slabs: out[row*cols_out + c] = sum_s ws[s][row*cols_in + c].
+// Folded input BN (the GEMM ran on r, the layer's true input is y = r*s + h,
+// zero outside the image): dW[row][col] = s[ci]*raw + h[ci]*V(row, col) where
+// V is the sum of the output gradient over the pixels whose tap hits the image.
+//  conv  (mode 1, row = co, col = t*cin + ci):  V = db[co] - oob(co, t), oob
+//        from the border sums bs[8][cout] = {top, bot, left, right, 4 corners}.
+//  tconv (mode 2, row = tap*cout + co, col = ci): V = par[row] (parity sums).
+struct WFold {
+  int mode;  // 0 none, 1 conv3x3, 2 tconv2x2
+  int cin, cout;
+  const float* s;
+  const float* h;
+  const float* db;  // mode 1: [cout]
+  const float* v;   // mode 1: border sums [8][cout]; mode 2: parity sums [4*cout]
+};
+
+__device__ __forceinline__ float fold_v(const WFold& f, int row, int col) {
+  if (f.mode == 2) return f.v[row];
+  const int t = col / f.cin, r = t / 3, q = t - 3 * r;
+  const float* b = f.v;
+  const int C = f.cout, co = row;
+  float o = 0.f;
+  if (r == 0) o += b[0 * C + co];
+  if (r == 2) o += b[1 * C + co];
+  if (q == 0) o += b[2 * C + co];
+  if (q == 2) o += b[3 * C + co];
+  if (r == 0 && q == 0) o -= b[4 * C + co];
+  if (r == 0 && q == 2) o -= b[5 * C + co];
+  if (r == 2 && q == 0) o -= b[6 * C + co];
+  if (r == 2 && q == 2) o -= b[7 * C + co];
+  return f.db[co] - o;
+}
+
+// Sum the split slabs: out[row*cols_out + c] = sum_s ws[s][row*cols_in + c]
+// (then the folded-BN correction when f.mode != 0).
 __global__ void slab_reduce_kernel(const float* __restrict__ ws, long slab, int splits, int rows,
-                                   int cols_in, int cols_out, float* __restrict__ out) {
+                                   int cols_in, int cols_out, float* __restrict__ out, WFold f) {
   const long total = (long)rows * cols_out;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
@@ -274,6 +309,10 @@ __global__ void slab_reduce_kernel(const float* __restrict__ ws, long slab, int 
     const long src = (long)row * cols_in + c;
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += ws[(size_t)k * slab + src];
+    if (f.mode) {
+      const int ci = c % f.cin;
+      s = s * f.s[ci] + f.h[ci] * fold_v(f, row, c);
+    }
     out[i] = s;
   }
 }
@@ -326,17 +365,50 @@ void launch_any(const WgradArgs& a, int bm, int bn, hipStream_t s, dim3 grid) {
 #undef CNN_W
 }
 
+bool wgrad_v1() {
+  static const bool v1 = [] {
+    const char* e = getenv("CNNITMO_WGRAD_V1");
+    return e && atoi(e) == 1;
+  }();
+  return v1;
+}
+
+// bf16: the v2 kernel (igemm_wgrad2.hip); returns splits written, < 0 if not taken.
+int try_wgrad2(const WgradArgs& a, int tapdep, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (wgrad_v1()) return -1;
+  Wgrad2Args b;
+  memset(&b, 0, sizeof(b));
+  b.a = (const bf16*)a.a; b.a_ld = a.a_ld; b.a_off = a.a_off; b.ha = a.ha; b.wa = a.wa; b.a_scale = a.a_scale;
+  b.b = (const bf16*)a.b; b.b_ld = a.b_ld; b.b_off = a.b_off; b.hb = a.hb; b.wb = a.wb; b.b_scale = a.b_scale;
+  b.nimg = a.nimg; b.hg = a.hg; b.wg = a.wg; b.ntaps = a.ntaps;
+  b.ayc = a.ayc; b.axc = a.axc; b.byc = a.byc; b.bxc = a.bxc; b.a_tapdep = tapdep;
+  b.M = a.M; b.N = a.N; b.tap_stride = a.tap_stride; b.out_ld = a.out_ld;
+  return launch_wgrad2(b, ws, ws_bytes, s);
+}
+
 template <typename T>
 int run_wgrad(WgradArgs a, float* out_final, int rows, int cols_in, int cols_out, void* ws,
-              size_t ws_bytes, hipStream_t s, const char* what) {
+              size_t ws_bytes, hipStream_t s, const char* what, const WFold& fold, int tapdep = 0) {
   CNN_REQUIRE(a.M % 32 == 0 && a.N % 32 == 0, "%s: channel counts %d/%d must be multiples of 32",
               what, a.M, a.N);
   CNN_REQUIRE(a.a_ld % Vec16<T>::N == 0 && a.b_ld % Vec16<T>::N == 0 && a.b_off % Vec16<T>::N == 0,
               "%s: views must be 16-byte aligned", what);
   a.P = (long)a.nimg * a.hg * a.wg;
   CNN_REQUIRE(a.P > 0, "%s: empty", what);
-  Plan pl = make_plan<T>(a.P, a.M, a.N, a.ntaps);
   const long slab = (long)a.M * a.N * a.ntaps;
+  const long outn = (long)rows * cols_out;
+  const int rblocks = (int)std::min<long>((outn + 255) / 256, 4096);
+  if constexpr (std::is_same<T, bf16>::value) {
+    const int splits = try_wgrad2(a, tapdep, ws, ws_bytes, s);
+    if (splits > 0) {
+      int rc = cnnitmo_check_launch(what);
+      if (rc) return rc;
+      hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)ws, slab,
+                         splits, rows, cols_in, cols_out, out_final, fold);
+      return cnnitmo_check_launch(what);
+    }
+  }
+  Plan pl = make_plan<T>(a.P, a.M, a.N, a.ntaps);
   CNN_REQUIRE(ws && ws_bytes >= (size_t)pl.splits * slab * 4, "%s: workspace too small (%zu < %zu)",
               what, ws_bytes, (size_t)pl.splits * slab * 4);
   a.out = (float*)ws;
@@ -349,17 +421,17 @@ int run_wgrad(WgradArgs a, float* out_final, int rows, int cols_in, int cols_out
   launch_any<T>(a, pl.bm, pl.bn, s, dim3((unsigned)total));
   int rc = cnnitmo_check_launch(what);
   if (rc) return rc;
-  const long outn = (long)rows * cols_out;
-  const int blocks = (int)std::min<long>((outn + 255) / 256, 4096);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)ws, slab,
-                     pl.splits, rows, cols_in, cols_out, out_final);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)ws, slab,
+                     pl.splits, rows, cols_in, cols_out, out_final, fold);
   return cnnitmo_check_launch(what);
 }
 
 template <typename T>
 size_t ws_bytes_for(long P, int M, int N, int ntaps) {
   Plan pl = make_plan<T>(P, M, N, ntaps);
-  return (size_t)pl.splits * M * N * ntaps * 4;
+  size_t b = (size_t)pl.splits * M * N * ntaps * 4;
+  if (std::is_same<T, bf16>::value && !wgrad_v1()) b = std::max(b, wgrad2_ws_bytes(P, M, N, ntaps));
+  return b;
 }
 
 }  // namespace
@@ -380,9 +452,17 @@ extern "C" size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h
 
 extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
                                   const void* dz, int n, int h, int w, int cin, int cout,
-                                  float* dw, int dw_cols, void* workspace, size_t ws_bytes,
+                                  float* dw, int dw_cols, const float* fold_scale,
+                                  const float* fold_shift, const float* fold_db,
+                                  const float* fold_border, void* workspace, size_t ws_bytes,
                                   void* stream) {
   CNN_REQUIRE(ntaps == 9 || ntaps == 1, "conv_wgrad: ntaps must be 9 or 1");
+  WFold f{0, cin, cout, fold_scale, fold_shift, fold_db, fold_border};
+  if (fold_scale) {
+    CNN_REQUIRE(ntaps == 9 && fold_shift && fold_db && fold_border && (dw_cols <= 0 || dw_cols == 9 * cin),
+                "conv_wgrad: folded BN needs ntaps 9, shift, db and border sums");
+    f.mode = 1;
+  }
   WgradArgs a;
   memset(&a, 0, sizeof(a));
   a.a = dz; a.a_ld = cout; a.a_off = 0; a.ha = h; a.wa = w; a.a_scale = 1;
@@ -401,16 +481,22 @@ extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld,
   const int cols_out = dw_cols > 0 ? dw_cols : ntaps * cin;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == CNNITMO_BF16)
-    return run_wgrad<bf16>(a, dw, cout, ntaps * cin, cols_out, workspace, ws_bytes, s, "conv_wgrad");
+    return run_wgrad<bf16>(a, dw, cout, ntaps * cin, cols_out, workspace, ws_bytes, s, "conv_wgrad", f);
   if (dtype == CNNITMO_F32)
-    return run_wgrad<float>(a, dw, cout, ntaps * cin, cols_out, workspace, ws_bytes, s, "conv_wgrad");
+    return run_wgrad<float>(a, dw, cout, ntaps * cin, cols_out, workspace, ws_bytes, s, "conv_wgrad", f);
   cnnitmo_set_error("conv_wgrad: unsupported dtype %d", dtype);
   return CNNITMO_EUNSUPPORTED;
 }
 
 extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h,
-                                      int w, int cin, int cout, float* dk, void* workspace,
-                                      size_t ws_bytes, void* stream) {
+                                      int w, int cin, int cout, float* dk, const float* fold_scale,
+                                      const float* fold_shift, const float* fold_par,
+                                      void* workspace, size_t ws_bytes, void* stream) {
+  WFold f{0, cin, cout, fold_scale, fold_shift, nullptr, fold_par};
+  if (fold_scale) {
+    CNN_REQUIRE(fold_shift && fold_par, "tconv2x2_wgrad: folded BN needs shift and parity sums");
+    f.mode = 2;
+  }
   WgradArgs a;
   memset(&a, 0, sizeof(a));
   a.a = dout; a.a_ld = cout; a.a_off = 0; a.ha = 2 * h; a.wa = 2 * w; a.a_scale = 2;
@@ -427,9 +513,9 @@ extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout
   a.tap_stride = (long)cout * cin; a.out_ld = cin;
   hipStream_t s = (hipStream_t)stream;
   if (dtype == CNNITMO_BF16)
-    return run_wgrad<bf16>(a, dk, 4 * cout, cin, cin, workspace, ws_bytes, s, "tconv2x2_wgrad");
+    return run_wgrad<bf16>(a, dk, 4 * cout, cin, cin, workspace, ws_bytes, s, "tconv2x2_wgrad", f, 1);
   if (dtype == CNNITMO_F32)
-    return run_wgrad<float>(a, dk, 4 * cout, cin, cin, workspace, ws_bytes, s, "tconv2x2_wgrad");
+    return run_wgrad<float>(a, dk, 4 * cout, cin, cin, workspace, ws_bytes, s, "tconv2x2_wgrad", f);
   cnnitmo_set_error("tconv2x2_wgrad: unsupported dtype %d", dtype);
   return CNNITMO_EUNSUPPORTED;
 }

@@ -59,10 +59,11 @@ def workspace(nbytes, device="cuda"):
 
 
 # ---------------------------------------------------------------- convolutions
-def conv3x3_fwd(dt, x: View, wt, bias, out: View, flags=0, aff=None, stats=None):
+def conv3x3_fwd(dt, x: View, wt, bias, out: View, flags=0, aff=None, stats=None, border=None):
     sc, sh = aff if aff is not None else (None, None)
     call("cnnitmo_conv3x3_fwd", dt, x.ptr, x.ld, x.off, x.n, x.h, x.w, x.c, ptr(wt), ptr(bias),
-         out.c, out.ptr, out.ld, out.off, flags, ptr(sc), ptr(sh), ptr(stats), stream_ptr())
+         out.c, out.ptr, out.ld, out.off, flags, ptr(sc), ptr(sh), ptr(stats), ptr(border),
+         stream_ptr())
 
 
 def conv1tap_fwd(dt, cols, k, m, wt, bias, out: View, flags=0, aff=None, stats=None):
@@ -80,11 +81,14 @@ def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx: View):
          stream_ptr())
 
 
-def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0):
+def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0, fold=None):
+    """fold = (scale, shift, db, border_sums) for a folded input BN, else None."""
     nbytes = query("cnnitmo_wgrad_workspace_bytes", dt, x.n, x.h, x.w, x.c, cout, ntaps)
     ws = workspace(nbytes, dz.device)
+    fs, fh, fdb, fb = fold if fold is not None else (None,) * 4
     call("cnnitmo_conv_wgrad", dt, ntaps, x.ptr, x.ld, x.off, ptr(dz), x.n, x.h, x.w, x.c, cout,
-         ptr(dw), dw_cols, ws.data_ptr(), ws.numel(), stream_ptr())
+         ptr(dw), dw_cols, ptr(fs), ptr(fh), ptr(fdb), ptr(fb), ws.data_ptr(), ws.numel(),
+         stream_ptr())
 
 
 def im2col_c3(dt, x, n, h_valid, h, w, cols):
@@ -102,12 +106,14 @@ def tconv_dgrad(dt, dout, n, h, w, cout, kT, cin, dx):
     call("cnnitmo_tconv2x2_dgrad", dt, ptr(dout), n, h, w, cout, ptr(kT), cin, ptr(dx), stream_ptr())
 
 
-def tconv_wgrad(dt, x: View, dout, cout, dk):
+def tconv_wgrad(dt, x: View, dout, cout, dk, fold=None):
+    """fold = (scale, shift, parity_sums[4*cout]) for a folded input BN, else None."""
     assert x.ld == x.c and x.off == 0
     nbytes = query("cnnitmo_tconv2x2_wgrad_workspace_bytes", dt, x.n, x.h, x.w, x.c, cout)
     ws = workspace(nbytes, dout.device)
+    fs, fh, fp = fold if fold is not None else (None,) * 3
     call("cnnitmo_tconv2x2_wgrad", dt, x.ptr, ptr(dout), x.n, x.h, x.w, x.c, cout, ptr(dk),
-         ws.data_ptr(), ws.numel(), stream_ptr())
+         ptr(fs), ptr(fh), ptr(fp), ws.data_ptr(), ws.numel(), stream_ptr())
 
 
 def prep_conv3x3(dt, w32, cout, cin, wf, wflip):
@@ -122,10 +128,29 @@ def prep_c3(dt, w32, cout, wp):
     call("cnnitmo_prep_c3_weights", dt, ptr(w32), cout, ptr(wp), stream_ptr())
 
 
+def fold_conv3x3(dt, w32, b, scale, shift, cout, cin, wout, bout, border):
+    call("cnnitmo_fold_conv3x3", dt, ptr(w32), ptr(b), ptr(scale), ptr(shift), cout, cin, ptr(wout),
+         ptr(bout), ptr(border), stream_ptr())
+
+
+def fold_tconv(dt, k32, b, scale, shift, cout, cin, kout, bout):
+    call("cnnitmo_fold_tconv2x2", dt, ptr(k32), ptr(b), ptr(scale), ptr(shift), cout, cin, ptr(kout),
+         ptr(bout), stream_ptr())
+
+
+def border_rows(n):
+    return query("cnnitmo_border_rows", n)
+
+
+def border_sums(dt, dz, n, h, w, c, part):
+    call("cnnitmo_border_sums", dt, ptr(dz), n, h, w, c, ptr(part), stream_ptr())
+
+
 # ---------------------------------------------------------------- pooling
-def maxpool_fwd(dt, x: View, y, idx):
+def maxpool_fwd(dt, x: View, y, idx, aff=None):
+    sc, sh = aff if aff is not None else (None, None)
     call("cnnitmo_maxpool2x2_fwd", dt, x.ptr, x.ld, x.off, x.n, x.h, x.w, x.c, ptr(y), ptr(idx),
-         stream_ptr())
+         ptr(sc), ptr(sh), stream_ptr())
 
 
 def maxpool_bwd(dt, dy, idx, dx: View):
@@ -160,9 +185,17 @@ def bn_bwd_rows(p, c):
     return query("cnnitmo_bn_bwd_rows", p, c)
 
 
+def _rview(r, c):
+    """(ptr, ld, off) of a saved post-ReLU tensor given as a View or a contiguous [p][c] tensor."""
+    if isinstance(r, View):
+        return r.ptr, r.ld, r.off
+    return ptr(r), c, 0
+
+
 def bn_bwd_reduce(dt, dy: View, r, c, mean, inv, flags, seed, layer, part):
-    call("cnnitmo_bn_bwd_reduce", dt, dy.ptr, dy.ld, dy.off, ptr(r), dy.p, c, ptr(mean), ptr(inv),
-         flags, seed, layer, ptr(part), stream_ptr())
+    rp, rld, roff = _rview(r, c)
+    call("cnnitmo_bn_bwd_reduce", dt, dy.ptr, dy.ld, dy.off, rp, rld, roff, dy.p, c, ptr(mean),
+         ptr(inv), flags, seed, layer, ptr(part), stream_ptr())
 
 
 def bn_bwd_finalize(part, rows, c, count, gamma, mean, inv, dgamma, dbeta, coef):
@@ -172,8 +205,10 @@ def bn_bwd_finalize(part, rows, c, count, gamma, mean, inv, dgamma, dbeta, coef)
 
 
 def bn_bwd_apply(dt, dy: View, r, c, coef, flags, seed, layer, dz, part):
-    call("cnnitmo_bn_bwd_apply", dt, dy.ptr, dy.ld, dy.off, ptr(r), dy.p, c, ptr(coef), flags, seed,
-         layer, ptr(dz), ptr(part), stream_ptr())
+    """flags & L.PARITY: part columns are [4][c] split by (h&1, w&1) of dy's pixel."""
+    rp, rld, roff = _rview(r, c)
+    call("cnnitmo_bn_bwd_apply", dt, dy.ptr, dy.ld, dy.off, rp, rld, roff, dy.p, c, ptr(coef), flags,
+         seed, layer, dy.h, dy.w, ptr(dz), ptr(part), stream_ptr())
 
 
 def colsum(part, rows, cols, groups, out):
@@ -182,24 +217,27 @@ def colsum(part, rows, cols, groups, out):
 
 
 # ---------------------------------------------------------------- head / optimizer
-def head_fwd(dt, x: View, h_valid, wt, b, yhat):
-    call("cnnitmo_head_fwd", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b), ptr(yhat),
-         stream_ptr())
+def head_fwd(dt, x: View, h_valid, wt, b, yhat, aff=None):
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_head_fwd", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b), ptr(sc),
+         ptr(sh), ptr(yhat), stream_ptr())
 
 
-def head_fwd_bwd(dt, x: View, h_valid, wt, b, target, dx, part):
-    call("cnnitmo_head_fwd_bwd", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b),
-         ptr(target), ptr(dx), ptr(part), stream_ptr())
+def head_fwd_bwd(dt, x: View, h_valid, wt, b, target, dx, part, aff=None):
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_head_fwd_bwd", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b), ptr(sc),
+         ptr(sh), ptr(target), ptr(dx), ptr(part), stream_ptr())
 
 
 def head_rows(p):
     return query("cnnitmo_head_rows", p)
 
 
-def head_finalize(part, rows, cin, numel, loss_acc, dw, db):
+def head_finalize(part, rows, cin, numel, loss_acc, dw, db, aff=None):
+    sc, sh = aff if aff is not None else (None, None)
     ws = reduce_ws(rows, 5 + 3 * cin, part.device)
-    call("cnnitmo_head_finalize", ptr(part), rows, cin, float(numel), ptr(loss_acc), ptr(dw), ptr(db),
-         ws.data_ptr(), stream_ptr())
+    call("cnnitmo_head_finalize", ptr(part), rows, cin, float(numel), ptr(sc), ptr(sh),
+         ptr(loss_acc), ptr(dw), ptr(db), ws.data_ptr(), stream_ptr())
 
 
 def rmsprop(p, g, a, lr, rho, eps, grad_scale=1.0):

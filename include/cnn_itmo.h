@@ -48,10 +48,12 @@ extern "C" {
 #define CNNITMO_RELU 1   /* Activation('relu') after the conv (model.py:196,200) */
 #define CNNITMO_STATS 2  /* write per-tile BN partial sums (sum, sum of squares) */
 #define CNNITMO_AFFINE 4 /* y = v*scale[c] + shift[c] after ReLU (inference BN) */
+#define CNNITMO_BIAS_PER_COL 8 /* bias indexed by GEMM column (tconv: [4*cout], folded BN) */
 
 /* Flags for BN apply / backward. */
 #define CNNITMO_DROPOUT 1 /* Dropout(0.5), model.py:226,239 (train only) */
 #define CNNITMO_NO_BN 2   /* bwd: plain ReLU gradient, no BN (config-1 net)  */
+#define CNNITMO_PARITY 4  /* bwd apply: bias partials split by (h&1, w&1) -> [4][c] */
 
 int cnnitmo_version(void);
 const char* cnnitmo_last_error(void);
@@ -62,12 +64,16 @@ const char* cnnitmo_last_error(void);
  * out view: [n, h, w, cout] (ld, off).  flags: CNNITMO_RELU|STATS|AFFINE.
  * stat_part (STATS): [rows][2][cout] fp32, rows = cnnitmo_fwd_stat_rows(...).
  * aff_scale/aff_shift (AFFINE): [cout] fp32.
+ * border (nullable): [cout][8] zero-padding correction of a folded input BN
+ * (cnnitmo_fold_conv3x3): when x holds r and the conv's true input is
+ * y = r*s + h, pass wt/bias/border from the fold.
  * Requires cin % 32 == 0 (bf16) or % 16 == 0 (f32), cout % 32 == 0.
  */
 int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w,
                         int cin, const void* wt, const float* bias, int cout, void* out,
                         int out_ld, int out_off, int flags, const float* aff_scale,
-                        const float* aff_shift, float* stat_part, void* stream);
+                        const float* aff_shift, float* stat_part, const float* border,
+                        void* stream);
 
 /* Rows of the BN partial-sum buffer written by a forward conv over m output
  * pixels with ncols GEMM columns (cout for conv3x3, 4*cout for tconv2x2). */
@@ -87,7 +93,14 @@ size_t cnnitmo_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin, in
                                      int ntaps);
 int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
                        const void* dz, int n, int h, int w, int cin, int cout, float* dw,
-                       int dw_cols, void* workspace, size_t ws_bytes, void* stream);
+                       int dw_cols, const float* fold_scale, const float* fold_shift,
+                       const float* fold_db, const float* fold_border, void* workspace,
+                       size_t ws_bytes, void* stream);
+/* Folded input BN (x holds r, the conv's input is y = r*s + h, see
+ * cnnitmo_fold_conv3x3): pass fold_scale = s, fold_shift = h [cin], fold_db = the
+ * bias gradient [cout] and fold_border = the reduced border sums [8][cout] of dz
+ * (cnnitmo_border_sums + cnnitmo_colsum); dw is then the exact gradient w.r.t. W.
+ * All four NULL: plain weight gradient. */
 
 /* First layer (Cin=3): pack x [n,h_valid,w,3] fp32 into [n,h,w,32] dtype
  * columns k=(r*3+s)*3+c (k<27, zero pad; rows >= h_valid are zero), so that
@@ -117,8 +130,11 @@ int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h, int w, int
                            const void* kT, int cin, void* dx, void* stream);
 /* dk [2][2][cout][cin] fp32 (OVERWRITTEN) from x [n,h,w,cin], dout [n,2h,2w,cout]. */
 int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h, int w,
-                           int cin, int cout, float* dk, void* workspace, size_t ws_bytes,
-                           void* stream);
+                           int cin, int cout, float* dk, const float* fold_scale,
+                           const float* fold_shift, const float* fold_par, void* workspace,
+                           size_t ws_bytes, void* stream);
+/* fold_par: per-tap sums of dout [4][cout] (cnnitmo_bn_bwd_apply with
+ * CNNITMO_PARITY, reduced by cnnitmo_colsum); NULL trio = plain gradient. */
 size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin, int cout);
 
 /* Weight preparation (after every optimizer step): fp32 master -> dtype copies.
@@ -131,6 +147,25 @@ int cnnitmo_prep_tconv2x2_weights(int dtype, const float* k, int cout, int cin, 
                                   void* kT, void* stream);
 int cnnitmo_prep_c3_weights(int dtype, const float* w, int cout, void* w_packed, void* stream);
 
+/* BN folding (training): the consumer of a BN output y = r*s + h reads the
+ * stored post-ReLU r and folds the affine into its own weights instead of
+ * materialising y (removes one full read+write of every activation).
+ * conv3x3: w_out = W*s (dtype), bias_out[cout] = b + sum_t u_t and border[cout][8]
+ *   (u_t[co] = sum_ci W[co][t][ci]*h[ci]) for cnnitmo_conv3x3_fwd's border.
+ * tconv2x2: k_out = K*s, bias_out[4*cout] per (tap, co) -> CNNITMO_BIAS_PER_COL.
+ * scale/shift NULL = identity. */
+int cnnitmo_fold_conv3x3(int dtype, const float* w, const float* bias, const float* scale,
+                         const float* shift, int cout, int cin, void* w_out, float* bias_out,
+                         float* border, void* stream);
+int cnnitmo_fold_tconv2x2(int dtype, const float* k, const float* bias, const float* scale,
+                          const float* shift, int cout, int cin, void* k_out, float* bias_out,
+                          void* stream);
+/* Border partial sums of dz [n,h,w,c] (contiguous): rows cnnitmo_border_rows(n)
+ * of [8][c] = {row 0, row h-1, col 0, col w-1, 4 corners}; reduce with cnnitmo_colsum. */
+int cnnitmo_border_rows(int n);
+int cnnitmo_border_sums(int dtype, const void* dz, int n, int h, int w, int c, float* part,
+                        void* stream);
+
 /* ---------------------------------------------------------------------------
  * MaxPooling2D(pool_size=(2,2), strides=2) -- model.py:210,215,220,227.
  * fwd: x view [n,h,w,c] -> y [n,h/2,w/2,c] contiguous + argmax idx uint8 (0..3,
@@ -138,7 +173,9 @@ int cnnitmo_prep_c3_weights(int dtype, const float* w, int cout, void* w_packed,
  * bwd: dx view [n,h,w,c] += scatter of dy to the argmax (other entries untouched).
  */
 int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w,
-                           int c, void* y, uint8_t* idx, void* stream);
+                           int c, void* y, uint8_t* idx, const float* scale, const float* shift,
+                           void* stream);
+/* scale/shift (nullable, [c]): pool over x*scale + shift (a folded BN output). */
 int cnnitmo_maxpool2x2_bwd(int dtype, const void* dy, const uint8_t* idx, int n, int h, int w,
                            int c, void* dx, int dx_ld, int dx_off, void* stream);
 
@@ -173,15 +210,19 @@ int cnnitmo_bn_apply(int dtype, const void* r, long p, int c, const float* scale
  * the bias gradient db (written).  With CNNITMO_NO_BN: dz = [r>0]*dy. */
 int cnnitmo_bn_bwd_rows(long p, int c);
 int cnnitmo_bn_bwd_reduce(int dtype, const void* dy, int dy_ld, int dy_off, const void* r,
-                          long p, int c, const float* mean, const float* invstd, int flags,
+                          int r_ld, int r_off, long p, int c, const float* mean,
+                          const float* invstd, int flags,
                           uint64_t drop_seed, int drop_layer, float* part, void* stream);
 int cnnitmo_bn_bwd_finalize(const float* part, long rows, int c, double count,
                             const float* gamma, const float* mean, const float* invstd,
                             float* dgamma, float* dbeta, float* coef, void* workspace,
                             void* stream);
-int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off, const void* r, long p,
-                         int c, const float* coef, int flags, uint64_t drop_seed, int drop_layer,
-                         void* dz, float* part, void* stream);
+int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off, const void* r,
+                         int r_ld, int r_off, long p, int c, const float* coef, int flags,
+                         uint64_t drop_seed, int drop_layer, int h, int w, void* dz, float* part,
+                         void* stream);
+/* r view: (r_ld, r_off).  part columns: [c], or [4][c] by pixel parity with
+ * CNNITMO_PARITY (h, w = the spatial size, needed only then). */
 /* Column sums of partial rows -> out[groups-folded c] (fp32, written). */
 int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* out,
                    void* workspace, void* stream);
@@ -194,13 +235,18 @@ int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* ou
  * (= dz * W), and partials (loss sum, correct count, dW, db) into part;
  * cnnitmo_head_finalize reduces them into loss, acc, dw, db. */
 int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
-                     const float* wt, const float* b, float* yhat, void* stream);
+                     const float* wt, const float* b, const float* scale, const float* shift,
+                     float* yhat, void* stream);
 int cnnitmo_head_rows(long p);
 int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
-                         const float* wt, const float* b, const float* target, void* dx,
-                         float* part, void* stream);
-int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel, float* loss_acc,
-                          float* dw, float* db, void* workspace, void* stream);
+                         const float* wt, const float* b, const float* scale,
+                         const float* shift, const float* target, void* dx, float* part,
+                         void* stream);
+int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
+                          const float* scale, const float* shift, float* loss_acc, float* dw,
+                          float* db, void* workspace, void* stream);
+/* scale/shift (nullable, [cin]): x holds r and the head's input is r*scale +
+ * shift (folded BN); dx is then d/dy and dw the gradient w.r.t. the raw W. */
 
 /* ---------------------------------------------------------------------------
  * RMSprop (keras.optimizers.RMSprop defaults via compile('rmsprop'), model.py:281):

@@ -39,8 +39,11 @@ def test_header_exports_and_bindings(lib):
 
 def test_queries_without_gpu(lib):
     # pure host-side queries (no device calls)
+    # one row of partial sums per 256-pixel (v2) or 128-pixel (v1, N=32) tile
     assert lib.cnnitmo_fwd_stat_rows(1, 66846720, 64) == 66846720 // 256
-    assert lib.cnnitmo_fwd_stat_rows(1, 1000, 512) == 8
+    assert lib.cnnitmo_fwd_stat_rows(1, 1000, 512) == 4
+    assert lib.cnnitmo_fwd_stat_rows(1, 1000, 32) in (4, 8)
+    assert lib.cnnitmo_border_rows(32) == 32 * 16
     assert lib.cnnitmo_wgrad_workspace_bytes(1, 32, 1088, 1920, 96, 64, 9) > 0
     assert lib.cnnitmo_bn_bwd_rows(1000, 64) >= 1
 
@@ -48,7 +51,7 @@ def test_queries_without_gpu(lib):
 def test_invalid_shape_errors(lib):
     from cnn_itmo_amd import _lib
     # channels not a multiple of 32 -> EINVAL with a message, before any launch
-    rc = lib.cnnitmo_conv3x3_fwd(1, None, 8, 0, 1, 4, 4, 8, None, None, 20, None, 20, 0, 0, None, None, None, None)
+    rc = lib.cnnitmo_conv3x3_fwd(1, None, 8, 0, 1, 4, 4, 8, None, None, 20, None, 20, 0, 0, None, None, None, None, None)
     assert rc == _lib.C.c_int(-1).value or rc < 0
     assert b"multiple" in lib.cnnitmo_last_error()
 
