@@ -66,14 +66,12 @@ class KernelTimer:
 
     @staticmethod
     def fwd_name(dt, n):
+        """Kernel chosen by igemm_fwd.hip's dispatch for n GEMM columns (mirrors pick2/use_v1)."""
         t = "bf16" if dt == 1 else "f32"
-        if n >= 128 and n % 128 == 0:
-            tile = "128x128"
-        elif n % 64 == 0:
-            tile = "256x64"
-        else:
-            tile = "256x32"
-        return f"igemm_fwd_kernel<{t},{tile}>"
+        if n == 32 or os.environ.get("CNNITMO_FWD_V1") == "1":
+            return f"igemm_fwd_kernel<{t},256x32>"
+        bn = 128 if n % 128 == 0 else 64 if n % 64 == 0 else 96 if n % 96 == 0 else 32
+        return f"igemm_fwd2_kernel<{t},256x{bn}>"
 
     def _bracket(self, name, flops, fn, *a, **k):
         if not self.on:
@@ -111,17 +109,17 @@ class KernelTimer:
             fl = 2.0 * m * out.c * 27  # algorithmic K = 3x3x3 (the packed 32 has 5 zero columns)
             return self._bracket(self.fwd_name(dt, out.c), fl, o["conv1tap_fwd"], dt, cols, kk, m, wt, bias, out, *a, **k)
 
-        def conv_wgrad(dt, ntaps, x, dz, cout, dw, dw_cols=0):
+        def conv_wgrad(dt, ntaps, x, dz, cout, dw, dw_cols=0, fold=None):
             fl = 2.0 * x.p * cout * (27 if ntaps == 1 else 9 * x.c)
             t = "bf16" if dt == 1 else "f32"
-            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad_kernel + slab_reduce)", fl, o["conv_wgrad"],
-                                 dt, ntaps, x, dz, cout, dw, dw_cols)
+            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad2_kernel + slab_reduce)", fl, o["conv_wgrad"],
+                                 dt, ntaps, x, dz, cout, dw, dw_cols, fold)
 
-        def tconv_wgrad(dt, x, dout, cout, dk):
+        def tconv_wgrad(dt, x, dout, cout, dk, fold=None):
             fl = 2.0 * x.p * 4 * cout * x.c
             t = "bf16" if dt == 1 else "f32"
-            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad_kernel + slab_reduce)", fl, o["tconv_wgrad"],
-                                 dt, x, dout, cout, dk)
+            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad2_kernel + slab_reduce)", fl, o["tconv_wgrad"],
+                                 dt, x, dout, cout, dk, fold)
 
         for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad), ("tconv_fwd", tconv_fwd),
                      ("tconv_dgrad", tconv_dgrad), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),

@@ -14,11 +14,24 @@ needs; anything else raises NotImplementedError at compile time):
   final Conv2D(3, 1, activation='sigmoid')       -> HeadStage (sigmoid + MSE + accuracy + grads)
 
 Training BN uses per-replica batch statistics (Keras semantics per process).
+
+BN folding (training): a BN without Dropout never materialises its output
+y = r*scale + shift.  The conv epilogue stores r = relu(conv) straight into
+the output Value (or its concat slice), the finalize writes scale/shift into
+the Value's per-channel coefficient buffer, and every consumer folds the
+affine: convs/tconvs fold it into their weights and bias each step
+(cnnitmo_fold_*, exact zero-padding border table), the pool and the head apply
+it on load, and the consumer's weight gradient gets the exact correction
+s*dW(r) + h*V (cnnitmo_conv_wgrad / tconv2x2_wgrad fold arguments).  This
+removes one read+write of every activation per step.  Dropout outputs stay
+materialised (identity coefficients).  CNNITMO_NO_FOLD=1 disables folding.
 Every parameter lives in one flat fp32 buffer laid out in REVERSE stage order,
 so backward produces gradients front-to-back -- the order the data-parallel
 bucketer (dist.py) all-reduces them in.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -43,6 +56,9 @@ class Value:
         self.gbuf = None
         self.ginit = False
         self.needs_grad = True
+        self.folded = False  # holds r; the true value is r*cs + ch (per channel)
+        self.cs = None  # coefficient buffers of the owner (persist across steps)
+        self.ch = None
 
     def owner(self):
         return self.place[0] if self.place else self
@@ -70,6 +86,18 @@ class Value:
             o.gbuf = (torch.zeros if zero else torch.empty)(n * o.h * o.w * o.c, dtype=dtype, device=device)
             if zero:
                 o.mark_grad()
+
+    def ensure_coef(self, device):
+        o = self.owner()
+        if o.cs is None:
+            o.cs = torch.ones(o.c, device=device, dtype=torch.float32)
+            o.ch = torch.zeros(o.c, device=device, dtype=torch.float32)
+
+    def coef(self):
+        """(scale, shift) [c] fp32 slices of the owner's coefficient buffers."""
+        o = self.owner()
+        off = self.place[1] if self.place else 0
+        return o.cs[off:off + self.c], o.ch[off:off + self.c]
 
     def mark_grad(self):
         self.ginit = True
@@ -124,6 +152,15 @@ class BlockStage(Stage):
         else:
             self.w_fwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
             self.w_bwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
+        self.foldable = self.kind != "c3in" and self.vin.folded
+        if self.foldable:  # per-step folded copies (training)
+            f32 = torch.float32
+            self.w_fold = torch.empty_like(self.w_fwd)
+            self.b_fold = torch.empty((4 if self.kind == "t2" else 1) * cout, dtype=f32, device=dev)
+            self.border = torch.empty(8 * cout, dtype=f32, device=dev) if self.kind == "c3" else None
+        if self.vout.folded:
+            self.vout.ensure_coef(dev)
+        self.fold_active = False
 
     def prep(self):
         e = self.eng
@@ -138,6 +175,19 @@ class BlockStage(Stage):
     def _conv(self, n, out_view, flags, aff=None, stats=None):
         e = self.eng
         bias = e.p(self.conv.name + "/bias")
+        if self.fold_active:
+            cs, ch = self.vin.coef()
+            w32 = e.p(self.conv.name + "/kernel")
+            if self.kind == "c3":
+                ops.fold_conv3x3(e.dt, w32, bias, cs, ch, self.cout, self.cin, self.w_fold, self.b_fold,
+                                 self.border)
+                ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fold, self.b_fold, out_view, flags, aff,
+                                stats, border=self.border)
+            else:
+                ops.fold_tconv(e.dt, w32, bias, cs, ch, self.cout, self.cin, self.w_fold, self.b_fold)
+                ops.tconv_fwd(e.dt, self.vin.view(n), self.w_fold, self.b_fold, out_view,
+                              flags | L.BIAS_PER_COL, aff, stats)
+            return
         if self.kind == "c3":
             ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
         elif self.kind == "c3in":
@@ -155,6 +205,7 @@ class BlockStage(Stage):
         e = self.eng
         cout = self.cout
         P = n * self.vout.h * self.vout.w
+        self.fold_active = training and self.foldable
         if self.kind == "c3in":
             self.cols = torch.empty(P * 32, dtype=e.tdtype, device=e.device)
             ops.im2col_c3(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.cols)
@@ -178,19 +229,26 @@ class BlockStage(Stage):
         m, ncols = self._gemm_rows(n)
         rows = ops.fwd_stat_rows(e.dt, m, ncols)
         stats = torch.empty(rows * 2 * ncols, device=e.device, dtype=torch.float32)
-        r = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
-        self._conv(n, ops.View(r, n, self.vout.h, self.vout.w, cout, cout, 0),
-                   (L.RELU if self.relu else 0) | L.STATS, stats=stats)
-        self.scale = torch.empty(cout, device=e.device, dtype=torch.float32)
-        self.shift = torch.empty(cout, device=e.device, dtype=torch.float32)
+        if self.vout.folded:  # r goes straight into the output (slice); consumers fold the BN
+            rview = out
+        else:
+            r = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
+            rview = ops.View(r, n, self.vout.h, self.vout.w, cout, cout, 0)
+        self._conv(n, rview, (L.RELU if self.relu else 0) | L.STATS, stats=stats)
+        if self.vout.folded:
+            self.scale, self.shift = self.vout.coef()
+        else:
+            self.scale = torch.empty(cout, device=e.device, dtype=torch.float32)
+            self.shift = torch.empty(cout, device=e.device, dtype=torch.float32)
         self.smean = torch.empty(cout, device=e.device, dtype=torch.float32)
         self.sinv = torch.empty(cout, device=e.device, dtype=torch.float32)
         ops.bn_fwd_finalize(stats, rows, cout, 4 if self.kind == "t2" else 1, P, g, b,
                             mm if e.update_moving else None, mv if e.update_moving else None,
                             bn.momentum, bn.epsilon, self.scale, self.shift, self.smean, self.sinv)
-        flags = L.DROPOUT if self.drop is not None else 0
-        ops.bn_apply(e.dt, r, P, cout, self.scale, self.shift, out, flags, e.drop_seed, self.drop_id)
-        self.r = r
+        if not self.vout.folded:
+            flags = L.DROPOUT if self.drop is not None else 0
+            ops.bn_apply(e.dt, r, P, cout, self.scale, self.shift, out, flags, e.drop_seed, self.drop_id)
+        self.r = rview
 
     def backward(self, n):
         e = self.eng
@@ -201,8 +259,9 @@ class BlockStage(Stage):
         dy = self.vout.gview(n)
         rows = ops.bn_bwd_rows(P, cout)
         dz = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
-        part2 = torch.empty(rows * cout, device=e.device, dtype=torch.float32)
-        flags = L.DROPOUT if self.drop is not None else 0
+        par = self.fold_active and self.kind == "t2"  # tconv wgrad fold needs per-tap sums of dz
+        part2 = torch.empty(rows * (4 if par else 1) * cout, device=e.device, dtype=torch.float32)
+        flags = (L.DROPOUT if self.drop is not None else 0) | (L.PARITY if par else 0)
         if self.bn is not None:
             bn = self.bn
             part = torch.empty(rows * 2 * cout, device=e.device, dtype=torch.float32)
@@ -215,15 +274,31 @@ class BlockStage(Stage):
         else:
             ops.bn_bwd_apply(e.dt, dy, self.r, cout, None, flags | L.NO_BN, e.drop_seed,
                              self.drop_id, dz, part2)
-        ops.colsum(part2, rows, cout, 1, e.g(self.conv.name + "/bias"))
+        db = e.g(self.conv.name + "/bias")
         dw = e.g(self.conv.name + "/kernel")
+        if par:
+            ops.colsum(part2, rows, 4 * cout, 4, db)
+            psum = torch.empty(4 * cout, device=e.device, dtype=torch.float32)
+            ops.colsum(part2, rows, 4 * cout, 1, psum)
+        else:
+            ops.colsum(part2, rows, cout, 1, db)
         if self.kind == "c3in":
             ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
                            dw, dw_cols=27)
         elif self.kind == "c3":
-            ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw)
+            fold = None
+            if self.fold_active:
+                h, w = self.vout.h, self.vout.w
+                brows = ops.border_rows(n)
+                bpart = torch.empty(brows * 8 * cout, device=e.device, dtype=torch.float32)
+                ops.border_sums(e.dt, dz, n, h, w, cout, bpart)
+                bsum = torch.empty(8 * cout, device=e.device, dtype=torch.float32)
+                ops.colsum(bpart, brows, 8 * cout, 1, bsum)
+                fold = self.vin.coef() + (db, bsum)
+            ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold)
         else:
-            ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw)
+            fold = self.vin.coef() + (psum,) if par else None
+            ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold)
         if self.vin.needs_grad:
             if self.vin.ginit:
                 raise NotImplementedError(f"{self.name}: input gradient would need accumulation")
@@ -253,7 +328,8 @@ class PoolStage(Stage):
             raise NotImplementedError("MaxPooling2D output feeding a concatenate")
         self.vout.ensure(n, e.tdtype, e.device)
         self.idx = torch.empty(n * self.vout.h * self.vout.w * self.vout.c, dtype=torch.uint8, device=e.device)
-        ops.maxpool_fwd(e.dt, self.vin.view(n), self.vout.buf, self.idx)
+        aff = self.vin.coef() if training and self.vin.folded else None
+        ops.maxpool_fwd(e.dt, self.vin.view(n), self.vout.buf, self.idx, aff)
 
     def backward(self, n):
         e = self.eng
@@ -295,16 +371,18 @@ class HeadStage(Stage):
         rows = ops.head_rows(n * self.vin.h * self.vin.w)
         part = torch.empty(rows * (5 + 3 * self.cin), device=e.device, dtype=torch.float32)
         dx = self.vin.gview(n)
+        aff = self.vin.coef() if e.training and self.vin.folded else None
         ops.head_fwd_bwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
-                         e.p(self.name + "/bias"), target, dx.buf, part)
+                         e.p(self.name + "/bias"), target, dx.buf, part, aff)
         ops.head_finalize(part, rows, self.cin, n * e.h_valid * self.vin.w * 3, loss_acc,
-                          e.g(self.name + "/kernel"), e.g(self.name + "/bias"))
+                          e.g(self.name + "/kernel"), e.g(self.name + "/bias"), aff)
         self.vin.mark_grad()
 
 
 # ---------------------------------------------------------------------------
-def compile_graph(model):
-    """Turn the Keras layer graph into an ordered list of stages."""
+def compile_graph(model, fold=True):
+    """Turn the Keras layer graph into an ordered list of stages.  fold: keep BN
+    outputs (without Dropout) unmaterialised in training (see module doc)."""
     layers = model.layers
     cons = {}
     for l in layers:
@@ -373,6 +451,7 @@ def compile_graph(model):
             else:
                 kind = "c3"
             vout = Value(t.layer.name, t.shape)
+            vout.folded = fold and bn is not None and drop is None
             values[id(t)] = vout
             st = BlockStage(kind, l, relu, bn, drop, drop_id, values[id(x)], vout)
             stages.append(st)
@@ -393,6 +472,7 @@ def compile_graph(model):
                 vout.members.append(v)
                 off += v.c
                 vins.append(v)
+            vout.folded = any(v.folded for v in vins)
             stages.append(ConcatStage(l, vins, vout))
         else:
             raise NotImplementedError(f"{l.name} ({type(l).__name__}) outside a fusable pattern")
@@ -432,7 +512,8 @@ class Engine:
         self.dtype_name = dtype
         self.dt, self.tdtype = ops.DTYPES[dtype]
         self.device = torch.device(device)
-        self.stages = compile_graph(model)
+        self.stages = compile_graph(model, fold=os.environ.get("CNNITMO_NO_FOLD", "0") != "1")
+        self.training = False
         self.h_valid = None
         self.update_moving = True
         self.drop_seed = 0
@@ -514,6 +595,7 @@ class Engine:
     def forward(self, x, training=False):
         n = self._input(x)
         self.prepare_weights()
+        self.training = training
         for st in self.stages[:-1]:
             st.forward(n, training)
         return n

@@ -1,0 +1,194 @@
+"""BN-folding parity (engine.py module doc): every consumer of a folded BN
+output reads the stored post-ReLU r and folds y = r*s + h itself.  Each test
+runs the folded kernels on r and compares with the oracle applied to the
+materialised y (fp64, zero padding on y), with the same tolerances as
+test_gpu_ops.py: fp32 1e-4, bf16 1.5e-2 of the output scale."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from oracle import unet_ref as R  # noqa: E402
+from tests.test_gpu_ops import DT, TDT, close, dev, host, rnd  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cnn_itmo_amd import _lib as L
+    L.load()
+
+
+def cu(a):
+    return torch.tensor(np.ascontiguousarray(a), dtype=torch.float32).cuda()
+
+
+def affine(rng, c, neg=False):
+    s = rng.uniform(0.3, 2.0, c)
+    if neg:
+        s *= np.where(rng.uniform(size=c) < 0.3, -1.0, 1.0)
+    return s.astype(np.float32), rng.standard_normal(c).astype(np.float32)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 8, 12), (64, 128, 5, 7), (96, 64, 1, 6), (32, 64, 6, 1),
+                                          (128, 256, 3, 4)])
+def test_conv3x3_folded_fwd_wgrad(dt, cin, cout, H, W):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin * 7 + cout + H)
+    N, ld, off = 2, cin + 32, 32  # r lives in a concat slice
+    rb = np.maximum(rng.standard_normal((N, H, W, ld)), 0).astype(np.float32)
+    w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    s, h = affine(rng, cin)
+    d = DT[dt]
+    rr = rnd(rb, dt)[..., off:]
+    y = rr * s + h
+    zref = R.conv2d_same(y, w.astype(np.float64), b)
+    wout = torch.empty(w.size, dtype=TDT[dt], device="cuda")
+    bout, border = torch.empty(cout, device="cuda"), torch.empty(cout, 8, device="cuda")
+    ops.fold_conv3x3(d, cu(w), cu(b), cu(s), cu(h), cout, cin, wout, bout, border)
+    rv = ops.View(dev(rb, dt).reshape(-1), N, H, W, cin, ld, off)
+    out = ops.new_view(N, H, W, cout, TDT[dt])
+    rows = ops.fwd_stat_rows(d, N * H * W, cout)
+    stats = torch.zeros(rows, 2, cout, device="cuda")
+    ops.conv3x3_fwd(d, rv, wout, bout, out, flags=1 | 2, stats=stats, border=border)
+    torch.cuda.synchronize()
+    close(host(out.buf).reshape(N, H, W, cout), np.maximum(zref, 0), dt, "folded fwd")
+    # weight gradient w.r.t. W from r + the fold correction
+    dz = rng.standard_normal((N, H, W, cout)).astype(np.float32)
+    dzr = rnd(dz, dt)
+    _, dw_ref, db_ref = R.conv2d_same_bwd(y, w.astype(np.float64), dzr, need_dx=False)
+    dzt = dev(dz, dt)
+    db = cu(dzr.reshape(-1, cout).sum(0))
+    brows = ops.border_rows(N)
+    bpart = torch.empty(brows, 8, cout, device="cuda")
+    ops.border_sums(d, dzt, N, H, W, cout, bpart)
+    bsum = torch.empty(8, cout, device="cuda")
+    ops.colsum(bpart, brows, 8 * cout, 1, bsum)
+    want_b = np.stack([dzr[:, 0].sum((0, 1)), dzr[:, -1].sum((0, 1)), dzr[:, :, 0].sum((0, 1)),
+                       dzr[:, :, -1].sum((0, 1)), dzr[:, 0, 0].sum(0), dzr[:, 0, -1].sum(0),
+                       dzr[:, -1, 0].sum(0), dzr[:, -1, -1].sum(0)])
+    dw = torch.empty(cout, 3, 3, cin, device="cuda")
+    ops.conv_wgrad(d, 9, rv, dzt, cout, dw, fold=(cu(s), cu(h), db, bsum))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(host(bsum), want_b, rtol=1e-4, atol=1e-3)
+    close(host(dw), dw_ref, dt, "folded wgrad")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("cin,cout,H,W", [(64, 32, 3, 5), (128, 64, 4, 4), (512, 256, 2, 3)])
+def test_tconv_folded_fwd_wgrad(dt, cin, cout, H, W):
+    from cnn_itmo_amd import ops
+    from cnn_itmo_amd import _lib as L
+    rng = np.random.default_rng(cin + 11)
+    N = 2
+    r = np.maximum(rng.standard_normal((N, H, W, cin)), 0).astype(np.float32)
+    k = (rng.standard_normal((2, 2, cout, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    s, h = affine(rng, cin)
+    d = DT[dt]
+    y = rnd(r, dt) * s + h
+    ref = np.maximum(R.tconv2x2s2(y, k.astype(np.float64), b), 0)
+    kout = torch.empty(k.size, dtype=TDT[dt], device="cuda")
+    bout = torch.empty(4 * cout, device="cuda")
+    ops.fold_tconv(d, cu(k), cu(b), cu(s), cu(h), cout, cin, kout, bout)
+    xv = ops.View(dev(r, dt).reshape(-1), N, H, W, cin, cin)
+    out = ops.new_view(N, 2 * H, 2 * W, cout, TDT[dt])
+    ops.tconv_fwd(d, xv, kout, bout, out, flags=L.RELU | L.BIAS_PER_COL)
+    torch.cuda.synchronize()
+    close(host(out.buf).reshape(ref.shape), ref, dt, "folded tconv fwd")
+    dout = rng.standard_normal((N, 2 * H, 2 * W, cout)).astype(np.float32)
+    dor = rnd(dout, dt)
+    _, dk_ref, _ = R.tconv2x2s2_bwd(y, k.astype(np.float64), dor)
+    par = np.stack([dor[:, i::2, j::2].sum((0, 1, 2)) for i in (0, 1) for j in (0, 1)])
+    dk = torch.empty(2, 2, cout, cin, device="cuda")
+    ops.tconv_wgrad(d, xv, dev(dout, dt), cout, dk, fold=(cu(s), cu(h), cu(par)))
+    torch.cuda.synchronize()
+    close(host(dk), dk_ref, dt, "folded tconv wgrad")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_bn_bwd_parity_partials_and_r_view(dt):
+    """bn_bwd_apply with CNNITMO_PARITY: per-(h&1, w&1) sums of dz; r read from a view."""
+    from cnn_itmo_amd import ops
+    from cnn_itmo_amd import _lib as L
+    rng = np.random.default_rng(12)
+    N, H, W, C, ld, off = 2, 6, 10, 64, 96, 32
+    rb = np.maximum(rng.standard_normal((N, H, W, ld)), 0).astype(np.float32)
+    dy = rng.standard_normal((N, H, W, C)).astype(np.float32)
+    d = DT[dt]
+    P = N * H * W
+    rv = ops.View(dev(rb, dt).reshape(-1), N, H, W, C, ld, off)
+    dyv = ops.View(dev(dy, dt).reshape(-1), N, H, W, C, C)
+    rows = ops.bn_bwd_rows(P, C)
+    part = torch.empty(rows, 4, C, device="cuda")
+    dz = torch.empty(P * C, dtype=TDT[dt], device="cuda")
+    ops.bn_bwd_apply(d, dyv, rv, C, None, L.NO_BN | L.PARITY, 0, 0, dz, part)
+    db, par = torch.empty(C, device="cuda"), torch.empty(4, C, device="cuda")
+    ops.colsum(part, rows, 4 * C, 4, db)
+    ops.colsum(part, rows, 4 * C, 1, par)
+    dz_ref = rnd(dy, dt) * (rnd(rb, dt)[..., off:] > 0)
+    dzr = rnd(dz_ref, dt)
+    par_ref = np.stack([dzr[:, i::2, j::2].sum((0, 1, 2)) for i in (0, 1) for j in (0, 1)])
+    torch.cuda.synchronize()
+    close(host(dz).reshape(dz_ref.shape), dz_ref, dt, "dz")
+    np.testing.assert_allclose(host(par), par_ref, rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(host(db), par_ref.sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_maxpool_affine(dt):
+    """Pool over y = r*s + h with some negative scales (max of y is not max of r)."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(13)
+    N, H, W, C, ld, off = 2, 6, 8, 64, 96, 32
+    rb = np.maximum(rng.standard_normal((N, H, W, ld)), 0).astype(np.float32)
+    s, h = affine(rng, C, neg=True)
+    d = DT[dt]
+    xv = ops.View(dev(rb, dt).reshape(-1), N, H, W, C, ld, off)
+    y = torch.empty(N * H // 2 * W // 2 * C, dtype=TDT[dt], device="cuda")
+    idx = torch.empty(N * H // 2 * W // 2 * C, dtype=torch.uint8, device="cuda")
+    ops.maxpool_fwd(d, xv, y, idx, aff=(cu(s), cu(h)))
+    # the kernel computes y in fp32 from the stored r
+    yin = (rnd(rb, dt)[..., off:].astype(np.float32) * s + h).astype(np.float64)
+    yr, ir = R.maxpool2x2(yin)
+    torch.cuda.synchronize()
+    close(host(y).reshape(yr.shape), yr, dt, "pool affine")
+    assert np.array_equal(idx.cpu().numpy().reshape(ir.shape), ir)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_head_folded(dt):
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(14)
+    N, Hv, H, W, C = 2, 7, 8, 16, 64
+    r = np.maximum(rng.standard_normal((N, H, W, C)), 0).astype(np.float32)
+    w = (rng.standard_normal((3, C)) * 0.2).astype(np.float32)
+    b = rng.standard_normal(3).astype(np.float32)
+    s, h = affine(rng, C)
+    t = rng.uniform(size=(N, Hv, W, 3)).astype(np.float32)
+    d = DT[dt]
+    xv = ops.View(dev(r, dt).reshape(-1), N, H, W, C, C)
+    aff = (cu(s), cu(h))
+    yh = torch.empty(N, Hv, W, 3, device="cuda")
+    ops.head_fwd(d, xv, Hv, cu(w), cu(b), yh, aff=aff)
+    y = (rnd(r, dt) * s + h)[:, :Hv]
+    yref = R.sigmoid(y @ w.T.astype(np.float64) + b)
+    rows = ops.head_rows(N * H * W)
+    part = torch.empty(rows, 5 + 3 * C, device="cuda")
+    dx = torch.empty(N * H * W * C, dtype=TDT[dt], device="cuda")
+    ops.head_fwd_bwd(d, xv, Hv, cu(w), cu(b), cu(t), dx, part, aff=aff)
+    la, dw, db = torch.empty(2, device="cuda"), torch.empty(3, C, device="cuda"), torch.empty(3, device="cuda")
+    ops.head_finalize(part, rows, C, N * Hv * W * 3, la, dw, db, aff=aff)
+    dz = R.mse_grad_z(yref, t)
+    dx_ref = np.zeros((N, H, W, C))
+    dx_ref[:, :Hv] = dz @ w.astype(np.float64)
+    torch.cuda.synchronize()
+    close(yh.cpu().numpy(), yref, "f32", "yhat")
+    assert abs(la[0].item() - R.mse(yref, t)) < 1e-5
+    close(host(dw) * 1e3, dz.reshape(-1, 3).T @ y.reshape(-1, C) * 1e3, "f32", "head dw")
+    close(host(db) * 1e3, dz.reshape(-1, 3).sum(0) * 1e3, "f32", "head db")
+    close(host(dx).reshape(dx_ref.shape) * 1e3, dx_ref * 1e3, dt, "head dx")

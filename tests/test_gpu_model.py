@@ -181,12 +181,19 @@ def test_unet_two_steps_and_determinism():
         outs.append((l1, l2, eng.params.cpu().numpy()))
     assert np.array_equal(outs[0][2], outs[1][2])
     P = build_unet((32, 32, 3), "float32", seed=5).named_weights()
-    net = R.UNetRef(P)
-    acc = {}
-    r1 = net.train_step(x, t, acc, seed=1)
-    r2 = net.train_step(x, t, acc, seed=2)
-    assert abs(outs[0][0][0] - r1[0]) <= 1e-5 * r1[0]
-    assert abs(outs[0][1][0] - r2[0]) <= 1e-3 * r2[0]
+    ref = {}
+    for dt in (np.float64, np.float32):
+        net = R.UNetRef(P, dt)
+        acc = {}
+        ref[dt] = (net.train_step(x.astype(dt), t.astype(dt), acc, seed=1)[0],
+                   net.train_step(x.astype(dt), t.astype(dt), acc, seed=2)[0])
+    r1, r2 = ref[np.float64]
+    assert abs(outs[0][0][0] - r1) <= 1e-5 * r1
+    # the first RMSprop step is sign-like (|update| ~ lr/sqrt(1-rho) for every weight), so the
+    # second loss inherits the sign noise of near-zero gradients: calibrate on numpy-fp32's own
+    # deviation from fp64 (1.4e-3 relative on this case).
+    floor = abs(ref[np.float32][1] - r2)
+    assert abs(outs[0][1][0] - r2) <= max(1e-3 * r2, 3 * floor), (outs[0][1][0], r2, ref[np.float32][1])
 
 
 def test_tiny_net_config1_parity():
