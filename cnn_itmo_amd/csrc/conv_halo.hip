@@ -1,0 +1,375 @@
+// 3x3 'same' convolution (forward and input-gradient) for the high-resolution,
+// few-channel layers of the U-Net (enc1b, enc2a/b, dec8, dec9: 32..192 channels
+// at 1920x1088 and 960x544), bf16.
+//
+// The implicit GEMM of igemm_fwd2.hip gathers A once per tap, so every input
+// pixel crosses L2 -> LDS nine times; with few channels per pixel that re-read,
+// not the MFMA, bounds those layers.  Here a workgroup owns a 4 x 64 tile of
+// output pixels and stages its (4+2) x (64+2) input halo ONCE per 32-channel
+// chunk; the nine taps are nine shifted windows of the same LDS image:
+//   A fragment (tap r,s; output row y, 16 columns x0..x0+15) =
+//       patch rows (y+r)*66 + x0+s .. +15   (consecutive LDS rows, any start)
+//   B fragment (tap t; 16 output channels) = wstage rows t*BN + j*16 .. +15
+// LDS rows are 64 B (32 bf16); piece c of row q is stored at piece
+// c ^ (((q >> 2) & 1) << 1), which keeps every ds_read_b128 lane group
+// conflict-free for windows starting at ANY row (tools: brute-force check in
+// DESIGN.md).  Operands arrive by global_load_lds_dwordx4 (lane-linear LDS
+// image, swizzle applied to the source piece).
+//
+// Persistent grid: one workgroup per CU walks a contiguous range of
+// (tile, column-block) items, tiles ordered image -> column strip -> row so the
+// next tile's halo rows are the previous tile's last rows (L2 hits).  A 2-stage
+// LDS ring overlaps the loads of item t+1 with the MFMAs of item t; the epilogue
+// (bias, ReLU, inference BN affine, folded-BN border correction, BN partial
+// sums: the same semantics as igemm_fwd2) stages each wave's 64 x BN tile in
+// the stage it just consumed and stores 16-byte rows.
+#include "igemm_common.h"
+
+namespace {
+
+__device__ __attribute__((aligned(256))) unsigned char h_zero_page[256] = {0};
+
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void glds16(const void* gsrc, const char* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(a) : "m0");
+}
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+constexpr int TH = 4, TW = 64;             // output tile
+constexpr int PW = TW + 2, PROWS = (TH + 2) * PW;  // 6 x 66 halo
+constexpr int NWAVE = 4, NT = NWAVE * 64;
+constexpr int P_INSTR = 28;                 // ceil(396 / 16) padded to a multiple of NWAVE
+static_assert(P_INSTR * 16 >= PROWS && P_INSTR % NWAVE == 0, "patch loads");
+
+__device__ __forceinline__ int hswz(int row, int piece) {
+  return (row << 6) + ((piece ^ (((row >> 2) & 1) << 1)) << 4);
+}
+
+template <int BN>
+struct HaloCfg {
+  static constexpr int FN = BN / 16;
+  static constexpr int B_ROWS = 9 * BN;
+  static constexpr int B_INSTR = ((B_ROWS + 15) / 16 + NWAVE - 1) / NWAVE * NWAVE;
+  static constexpr int PATCH = P_INSTR * 1024;
+  static constexpr int STAGE = PATCH + B_INSTR * 1024;
+  static constexpr int CLD = BN + 8;  // C staging row (bf16), per wave 64 rows
+  static constexpr int C_BYTES = NWAVE * 64 * CLD * 2;
+  static constexpr int SMEM = 2 * STAGE;
+  static_assert(C_BYTES + NWAVE * BN * 8 <= STAGE, "epilogue staging must fit in one stage");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+struct HaloArgs {
+  FwdArgs f;
+  int tiles_x, tiles_y;  // per image
+  long npairs;           // tiles * nblocks
+  long per_block;        // contiguous items per workgroup
+  int nchunks;           // cin / 32
+};
+
+template <int BN>
+__global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
+  using C = HaloCfg<BN>;
+  constexpr int FN = C::FN, STAGE = C::STAGE;
+  constexpr int CPR = BN / 8;  // 16-byte output pieces per pixel
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  const FwdArgs& p = h.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long q0 = (long)blockIdx.x * h.per_block;
+  const long q1 = q0 + h.per_block < h.npairs ? q0 + h.per_block : h.npairs;
+  if (q0 >= q1) return;
+  const int nch = h.nchunks;
+  const long T = (q1 - q0) * nch;
+  const bf16* __restrict__ X = (const bf16*)p.a;
+  const bf16* __restrict__ Wt = (const bf16*)p.b;
+  const int K = 9 * p.cin;
+  const int tpi = h.tiles_x * h.tiles_y;
+
+  // (img, ty, tx, nb) of item q: ty fastest so consecutive tiles share halo rows
+  auto decode = [&](long ql, int& img, int& y0, int& x0, int& nb) {
+    const int q = (int)ql;  // npairs < 2^31 (checked by the launcher)
+    const int tile = q / p.nblocks;
+    nb = q - tile * p.nblocks;
+    img = tile / tpi;
+    const int rem = tile - img * tpi;
+    const int txi = rem / h.tiles_y;
+    y0 = (rem - txi * h.tiles_y) * TH;
+    x0 = txi * TW;
+  };
+  // incremental position of the item being issued (no divisions in the loop)
+  struct Pos {
+    int img, y0, x0, nb, ch;
+  };
+  Pos ip;
+  decode(q0, ip.img, ip.y0, ip.x0, ip.nb);
+  ip.ch = 0;
+  auto step = [&](Pos& s) {
+    if (++s.ch < nch) return;
+    s.ch = 0;
+    if (++s.nb < p.nblocks) return;
+    s.nb = 0;
+    s.y0 += TH;
+    if (s.y0 < p.ho) return;
+    s.y0 = 0;
+    s.x0 += TW;
+    if (s.x0 < p.wo) return;
+    s.x0 = 0;
+    ++s.img;
+  };
+
+  // per-lane load geometry, fixed for the whole launch: one glds instruction =
+  // 16 LDS rows x 4 pieces of 16 B; lane -> (row, piece), source piece swizzled
+  const int lrow = lane >> 2, lpc = lane & 3;
+  constexpr int NPI = P_INSTR / NWAVE, NBI = C::B_INSTR / NWAVE;
+  int ppy[NPI], ppx[NPI];
+  long poff[NPI];  // element offset of the lane's source piece from the tile origin
+#pragma unroll
+  for (int i = 0; i < NPI; ++i) {
+    const int row = (wave * NPI + i) * 16 + lrow;
+    const int piece = lpc ^ (((row >> 2) & 1) << 1);
+    const int py = row / PW, px = row - (row / PW) * PW;
+    ppy[i] = row < PROWS ? py : -(1 << 29);  // padded rows: never in bounds, never loaded
+    ppx[i] = px;
+    poff[i] = ((long)(py - 1) * p.ws + (px - 1)) * p.a_ld + piece * 8;
+  }
+  int boff[NBI];
+#pragma unroll
+  for (int i = 0; i < NBI; ++i) {
+    const int row = (wave * NBI + i) * 16 + lrow;  // = tap * BN + n
+    const int piece = lpc ^ (((row >> 2) & 1) << 1);
+    const int tap = row / BN, n = row - (row / BN) * BN;
+    boff[i] = row < C::B_ROWS ? n * K + tap * p.cin + piece * 8 : -1;
+  }
+
+  auto issue = [&](int buf) {
+    const Pos& s = ip;
+    char* Ps = smem + buf * STAGE;
+    char* Bs = Ps + C::PATCH;
+    const bf16* tb = X + ((size_t)((long)s.img * p.hs + s.y0) * p.ws + s.x0) * p.a_ld + p.a_off + s.ch * 32;
+    const bool interior = s.y0 >= 1 && s.y0 + TH < p.hs && s.x0 >= 1 && s.x0 + TW < p.ws;
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      const void* src = h_zero_page;
+      if (interior) {
+        if (ppy[i] >= 0) src = tb + poff[i];
+      } else {
+        const int yy = s.y0 + ppy[i] - 1, xx = s.x0 + ppx[i] - 1;
+        if ((unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws) src = tb + poff[i];
+      }
+      glds16(src, Ps + (wave * NPI + i) * 1024);
+    }
+    const bf16* bb = Wt + (size_t)s.nb * BN * K + s.ch * 32;
+#pragma unroll
+    for (int i = 0; i < NBI; ++i)
+      glds16(boff[i] >= 0 ? (const void*)(bb + boff[i]) : (const void*)h_zero_page, Bs + (wave * NBI + i) * 1024);
+  };
+
+  f32x4 acc[4][FN];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+
+  // fragment-read addresses: A window row = rbase + c with c = (y+r)*66 + 16i + s
+  // compile-time; the swizzle bit of (rbase + c) depends only on (c & 7), so the
+  // 8 residues are precomputed and c*64 becomes an immediate offset.
+  const int frow = lane & 15, fpc = lane >> 4;
+  const int rbase = wave * PW + frow;
+  int apre[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) apre[k] = rbase * 64 + ((fpc ^ ((((rbase + k) >> 2) & 1) << 1)) << 4);
+  const int bpre = frow * 64 + ((fpc ^ (((frow >> 2) & 1) << 1)) << 4);
+  auto compute = [&](int buf) {
+    const char* Ps = smem + buf * STAGE;
+    const char* Bs = Ps + C::PATCH;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int r = tap / 3, s = tap - 3 * (tap / 3);
+      uint4 af[4], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = r * PW + i * 16 + s;
+        af[i] = *reinterpret_cast<const uint4*>(Ps + apre[c & 7] + c * 64);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const uint4*>(Bs + bpre + (tap * BN + j * 16) * 64);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], af[i], bfr[j]);
+    }
+  };
+
+  const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE,
+             stats = p.flags & CNNITMO_STATS;
+  auto epilogue = [&](const Pos& e, int buf) {
+    const int img = e.img, y0 = e.y0, x0 = e.x0;
+    const int n0 = e.nb * BN;
+    const int oh = y0 + wave;
+    bf16* Cs = reinterpret_cast<bf16*>(smem + buf * STAGE) + wave * 64 * C::CLD;
+    float* red = reinterpret_cast<float*>(smem + buf * STAGE + C::C_BYTES);  // [NWAVE][BN][2]
+    float s1[FN], s2[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + j * 16 + (lane & 15);
+      const float bj = p.bias ? p.bias[n] : 0.f;
+      const float sj = aff ? p.aff_scale[n] : 1.f, hj = aff ? p.aff_shift[n] : 0.f;
+      const float* U = p.border ? p.border + (size_t)n * 8 : nullptr;
+      s1[j] = s2[j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int col = i * 16 + (lane >> 4) * 4 + r;  // pixel within the wave's row
+          float v = acc[i][j][r] + bj;
+          if (U) v -= border_corr(U, oh, x0 + col, p.ho, p.wo);
+          if (relu) v = fmaxf(v, 0.f);
+          if (aff) v = v * sj + hj;
+          s1[j] += v;
+          s2[j] += v * v;
+          Cs[col * C::CLD + j * 16 + (lane & 15)] = from_f32<bf16>(v);
+        }
+    }
+    if (stats) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        s1[j] += __shfl_xor(s1[j], 16, 64);
+        s1[j] += __shfl_xor(s1[j], 32, 64);
+        s2[j] += __shfl_xor(s2[j], 16, 64);
+        s2[j] += __shfl_xor(s2[j], 32, 64);
+      }
+      if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          red[(wave * BN + j * 16 + lane) * 2 + 0] = s1[j];
+          red[(wave * BN + j * 16 + lane) * 2 + 1] = s2[j];
+        }
+      }
+    }
+    __syncthreads();
+    if (stats && tid < BN) {
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < NWAVE; ++w) {
+        t1 += red[(w * BN + tid) * 2 + 0];
+        t2 += red[(w * BN + tid) * 2 + 1];
+      }
+      // one row per 256-pixel tile: tile index = ((img*H + y0)/4)*(W/64) + x0/64 (= m0/256)
+      const long tile = ((long)img * p.ho + y0) / TH * h.tiles_x + x0 / TW;
+      float* st = p.stats + (size_t)tile * 2 * p.N;
+      st[n0 + tid] = t1;
+      st[p.N + n0 + tid] = t2;
+    }
+    // each wave stores its 64 pixels x BN channels as 16-byte row pieces
+    bf16* __restrict__ O = (bf16*)p.out;
+    const long mrow = ((long)img * p.ho + oh) * p.wo + x0;
+#pragma unroll
+    for (int idx = lane; idx < 64 * CPR; idx += 64) {
+      const int col = idx / CPR, cc = idx - col * CPR;
+      const uint4 v = *reinterpret_cast<const uint4*>(Cs + col * C::CLD + cc * 8);
+      *reinterpret_cast<uint4*>(O + (size_t)(mrow + col) * p.out_ld + p.out_off + n0 + cc * 8) = v;
+    }
+    zero_acc();
+  };
+
+  // vmcnt retires in issue order: after an epilogue, the wave's CPR output stores
+  // (+2 BN-partial stores on wave 0) are younger than the loads of the next item,
+  // so the top-of-loop wait leaves exactly those in flight.
+  bool stored = false;
+  Pos ep = ip;  // position of the item being computed
+  issue(0);
+  step(ip);
+  for (long t = 0; t < T; ++t) {
+    if (!stored) wait_vm<0>();
+    else if (stats && wave == 0) wait_vm<CPR + 2>();
+    else wait_vm<CPR>();
+    stored = false;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < T) {
+      issue((int)((t + 1) & 1));
+      step(ip);
+    }
+    compute((int)(t & 1));
+    if (ep.ch == nch - 1) {
+      __syncthreads();  // every wave is done reading this stage: reuse it for the C tile
+      epilogue(ep, (int)(t & 1));
+      stored = true;
+    }
+    step(ep);
+  }
+}
+
+template <int BN>
+int launch_bn(const HaloArgs& h, hipStream_t s) {
+  // one workgroup per CU (LDS-limited); 256 CUs
+  hipLaunchKernelGGL((conv3x3_halo_kernel<BN>), dim3((unsigned)((h.npairs + h.per_block - 1) / h.per_block)),
+                     dim3(NT), 0, s, h);
+  return 0;
+}
+
+}  // namespace
+
+// Applicability: bf16, 3x3 taps at stride 1, whole 4 x 64 tiles, 32-channel chunks.
+int halo_bn_for(int N) {
+  if (N % 64 == 0) return 64;
+  if (N % 48 == 0) return 48;
+  if (N % 32 == 0) return 32;
+  return 0;
+}
+
+bool halo_handles(const FwdArgs& a) {
+  static const int mode = [] {
+    const char* e = getenv("CNNITMO_HALO");
+    return e ? atoi(e) : 1;
+  }();
+  if (!mode) return false;
+  return a.ntaps == 9 && a.scale == 1 && !a.scatter && a.hs == a.ho && a.ws == a.wo &&
+         a.ho % TH == 0 && a.wo % TW == 0 && a.cin % 32 == 0 && halo_bn_for(a.N) > 0 &&
+         a.a_ld % 8 == 0 && a.a_off % 8 == 0 && a.out_ld % 8 == 0 && a.out_off % 8 == 0 &&
+         (a.cin <= 256 || mode == 2);
+}
+
+int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
+  HaloArgs h;
+  h.f = a;
+  const int bn = halo_bn_for(a.N);
+  h.f.nblocks = a.N / bn;
+  h.tiles_x = a.wo / TW;
+  h.tiles_y = a.ho / TH;
+  h.nchunks = a.cin / 32;
+  const long tiles = (long)a.nimg * h.tiles_x * h.tiles_y;
+  h.npairs = tiles * h.f.nblocks;
+  CNN_REQUIRE(h.npairs * h.nchunks < (1L << 31), "%s: too many tiles", what);
+  int cus = 256;
+  {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      hipDeviceProp_t prop;
+      if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+        ncu = prop.multiProcessorCount;
+      if (ncu <= 0) ncu = 256;
+    }
+    cus = ncu;
+  }
+  h.per_block = (h.npairs + cus - 1) / cus;
+  CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
+  switch (bn) {
+    case 64: launch_bn<64>(h, s); break;
+    case 48: launch_bn<48>(h, s); break;
+    default: launch_bn<32>(h, s); break;
+  }
+  return cnnitmo_check_launch(what);
+}

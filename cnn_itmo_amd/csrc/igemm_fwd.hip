@@ -292,6 +292,7 @@ bool use_v1() {
 
 int dispatch(int dtype, const FwdArgs& a, void* stream, const char* what) {
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == CNNITMO_BF16 && halo_handles(a)) return launch_halo(a, s, what);
   if (!use_v1() && fwd2_handles(a.N)) {
     if (dtype == CNNITMO_BF16) return launch_fwd2<bf16>(a, s, what);
     if (dtype == CNNITMO_F32) return launch_fwd2<float>(a, s, what);

@@ -44,7 +44,10 @@ def close(got, want, dt, what=""):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-@pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 8, 12), (64, 128, 5, 7), (96, 64, 6, 10), (32, 256, 4, 4)])
+@pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 8, 12), (64, 128, 5, 7), (96, 64, 6, 10), (32, 256, 4, 4),
+                                          # whole 4x64 tiles: the halo kernel (bf16) for fwd and dgrad
+                                          (32, 32, 8, 64), (96, 64, 4, 128), (192, 128, 4, 64),
+                                          (64, 64, 12, 64), (32, 64, 12, 192)])
 def test_conv3x3_fwd_dgrad_wgrad(dt, cin, cout, H, W):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(cin + cout)
@@ -87,11 +90,31 @@ def test_conv3x3_fwd_dgrad_wgrad(dt, cin, cout, H, W):
     close(host(dw), dw_ref, dt, "wgrad")
 
 
+def test_conv3x3_halo_tall_frame():
+    """Halo kernel on a frame taller than 1024 rows (tile row offsets > 1000), bf16."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(21)
+    N, H, W, cin, cout = 1, 1032, 128, 32, 32
+    x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
+    w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    d = DT["bf16"]
+    wf = torch.empty(w.size, dtype=TDT["bf16"], device="cuda")
+    ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cin, wf, None)
+    out = ops.new_view(N, H, W, cout, TDT["bf16"])
+    ops.conv3x3_fwd(d, ops.View(dev(x, "bf16").reshape(-1), N, H, W, cin, cin), wf, torch.tensor(b).cuda(),
+                    out, flags=1)
+    ref = np.maximum(R.conv2d_same(rnd(x, "bf16"), rnd(w, "bf16"), b), 0)
+    torch.cuda.synchronize()
+    close(host(out.buf).reshape(ref.shape), ref, "bf16", "tall frame")
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-def test_conv_affine_inference_epilogue(dt):
+@pytest.mark.parametrize("H,W", [(6, 9), (4, 64)])
+def test_conv_affine_inference_epilogue(dt, H, W):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(3)
-    N, H, W, cin, cout = 1, 6, 9, 32, 64
+    N, cin, cout = 1, 32, 64
     x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
     w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
     b = rng.standard_normal(cout).astype(np.float32)
