@@ -89,13 +89,18 @@ class KernelTimer:
         o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_dgrad", "tconv_fwd", "tconv_dgrad",
                                            "conv1tap_fwd", "conv_wgrad", "tconv_wgrad")}
 
+        def kname(dt, n, h, w, cin, cout, dgrad):
+            return ops.query("cnnitmo_conv3x3_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
+
         def conv3x3_fwd(dt, x, wt, bias, out, *a, **k):
             fl = 2.0 * x.p * out.c * 9 * x.c
-            return self._bracket(self.fwd_name(dt, out.c), fl, o["conv3x3_fwd"], dt, x, wt, bias, out, *a, **k)
+            return self._bracket(kname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, o["conv3x3_fwd"], dt, x, wt, bias,
+                                 out, *a, **k)
 
         def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx):
             fl = 2.0 * n * h * w * cin * 9 * cout
-            return self._bracket(self.fwd_name(dt, cin), fl, o["conv3x3_dgrad"], dt, dz, n, h, w, cout, wflip, cin, dx)
+            return self._bracket(kname(dt, n, h, w, cin, cout, 1), fl, o["conv3x3_dgrad"], dt, dz, n, h, w, cout,
+                                 wflip, cin, dx)
 
         def tconv_fwd(dt, x, k_, bias, out, *a, **k):
             fl = 2.0 * x.p * 4 * out.c * x.c

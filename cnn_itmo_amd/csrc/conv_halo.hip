@@ -40,27 +40,40 @@ __device__ __forceinline__ void glds16(const void* gsrc, const char* lds) {
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-
-constexpr int TH = 4, TW = 64;             // output tile
-constexpr int PW = TW + 2, PROWS = (TH + 2) * PW;  // 6 x 66 halo
-constexpr int NWAVE = 4, NT = NWAVE * 64;
-constexpr int P_INSTR = 28;                 // ceil(396 / 16) padded to a multiple of NWAVE
-static_assert(P_INSTR * 16 >= PROWS && P_INSTR % NWAVE == 0, "patch loads");
+// s_waitcnt takes an immediate: dispatch a wave-uniform count (0..31)
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+  switch (n) {
+#define W1(k) case k: wait_vm<k>(); break;
+    W1(0) W1(1) W1(2) W1(3) W1(4) W1(5) W1(6) W1(7) W1(8) W1(9) W1(10) W1(11) W1(12) W1(13) W1(14) W1(15)
+    W1(16) W1(17) W1(18) W1(19) W1(20) W1(21) W1(22) W1(23) W1(24) W1(25) W1(26) W1(27) W1(28) W1(29)
+    W1(30) W1(31)
+#undef W1
+    default: wait_vm<0>(); break;
+  }
+}
 
 __device__ __forceinline__ int hswz(int row, int piece) {
   return (row << 6) + ((piece ^ (((row >> 2) & 1) << 1)) << 4);
 }
 
-template <int BN>
+// Tile TH x TW output pixels, one wave per output row (FM = TW/16 fragments),
+// BN output channels per item, ST-deep LDS ring.
+template <int TH, int TW, int BN, int ST>
 struct HaloCfg {
-  static constexpr int FN = BN / 16;
+  static constexpr int NWAVE = TH, NT = NWAVE * 64;
+  static constexpr int FM = TW / 16, FN = BN / 16;
+  static constexpr int PW = TW + 2, PROWS = (TH + 2) * PW;
+  static constexpr int P_INSTR = ((PROWS + 15) / 16 + NWAVE - 1) / NWAVE * NWAVE;
   static constexpr int B_ROWS = 9 * BN;
   static constexpr int B_INSTR = ((B_ROWS + 15) / 16 + NWAVE - 1) / NWAVE * NWAVE;
+  static constexpr int NPI = P_INSTR / NWAVE, NBI = B_INSTR / NWAVE;
   static constexpr int PATCH = P_INSTR * 1024;
   static constexpr int STAGE = PATCH + B_INSTR * 1024;
-  static constexpr int CLD = BN + 8;  // C staging row (bf16), per wave 64 rows
-  static constexpr int C_BYTES = NWAVE * 64 * CLD * 2;
-  static constexpr int SMEM = 2 * STAGE;
+  static constexpr int CLD = BN + 8;  // C staging row (bf16), per wave TW rows
+  static constexpr int C_BYTES = NWAVE * TW * CLD * 2;
+  static constexpr int SMEM = ST * STAGE;
+  static constexpr int SG = TH * TW / 256;  // BN-partial-sum rows per tile (256 pixels each)
+  static_assert(TH * TW % 256 == 0 && TW % 16 == 0, "tile");
   static_assert(C_BYTES + NWAVE * BN * 8 <= STAGE, "epilogue staging must fit in one stage");
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
@@ -73,10 +86,11 @@ struct HaloArgs {
   int nchunks;           // cin / 32
 };
 
-template <int BN>
-__global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
-  using C = HaloCfg<BN>;
-  constexpr int FN = C::FN, STAGE = C::STAGE;
+template <int TH, int TW, int BN, int ST>
+__global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h) {
+  using C = HaloCfg<TH, TW, BN, ST>;
+  constexpr int NWAVE = C::NWAVE, FM = C::FM, FN = C::FN, STAGE = C::STAGE, PW = C::PW;
+  constexpr int NPI = C::NPI, NBI = C::NBI;
   constexpr int CPR = BN / 8;  // 16-byte output pieces per pixel
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
@@ -91,24 +105,23 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
   const int K = 9 * p.cin;
   const int tpi = h.tiles_x * h.tiles_y;
 
-  // (img, ty, tx, nb) of item q: ty fastest so consecutive tiles share halo rows
-  auto decode = [&](long ql, int& img, int& y0, int& x0, int& nb) {
-    const int q = (int)ql;  // npairs < 2^31 (checked by the launcher)
-    const int tile = q / p.nblocks;
-    nb = q - tile * p.nblocks;
-    img = tile / tpi;
-    const int rem = tile - img * tpi;
-    const int txi = rem / h.tiles_y;
-    y0 = (rem - txi * h.tiles_y) * TH;
-    x0 = txi * TW;
-  };
-  // incremental position of the item being issued (no divisions in the loop)
+  // position of an item: (img, tile row, tile column, column block, chunk);
+  // tile rows fastest so consecutive tiles share halo rows
   struct Pos {
     int img, y0, x0, nb, ch;
   };
   Pos ip;
-  decode(q0, ip.img, ip.y0, ip.x0, ip.nb);
-  ip.ch = 0;
+  {
+    const int q = (int)q0;  // npairs < 2^31 (checked by the launcher)
+    const int tile = q / p.nblocks;
+    ip.nb = q - tile * p.nblocks;
+    ip.img = tile / tpi;
+    const int rem = tile - ip.img * tpi;
+    const int txi = rem / h.tiles_y;
+    ip.y0 = (rem - txi * h.tiles_y) * TH;
+    ip.x0 = txi * TW;
+    ip.ch = 0;
+  }
   auto step = [&](Pos& s) {
     if (++s.ch < nch) return;
     s.ch = 0;
@@ -126,7 +139,6 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
   // per-lane load geometry, fixed for the whole launch: one glds instruction =
   // 16 LDS rows x 4 pieces of 16 B; lane -> (row, piece), source piece swizzled
   const int lrow = lane >> 2, lpc = lane & 3;
-  constexpr int NPI = P_INSTR / NWAVE, NBI = C::B_INSTR / NWAVE;
   int ppy[NPI], ppx[NPI];
   long poff[NPI];  // element offset of the lane's source piece from the tile origin
 #pragma unroll
@@ -134,7 +146,7 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
     const int row = (wave * NPI + i) * 16 + lrow;
     const int piece = lpc ^ (((row >> 2) & 1) << 1);
     const int py = row / PW, px = row - (row / PW) * PW;
-    ppy[i] = row < PROWS ? py : -(1 << 29);  // padded rows: never in bounds, never loaded
+    ppy[i] = row < C::PROWS ? py : -(1 << 29);  // padded rows: never in bounds, never loaded
     ppx[i] = px;
     poff[i] = ((long)(py - 1) * p.ws + (px - 1)) * p.a_ld + piece * 8;
   }
@@ -170,16 +182,16 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
       glds16(boff[i] >= 0 ? (const void*)(bb + boff[i]) : (const void*)h_zero_page, Bs + (wave * NBI + i) * 1024);
   };
 
-  f32x4 acc[4][FN];
+  f32x4 acc[FM][FN];
   auto zero_acc = [&]() {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
 
-  // fragment-read addresses: A window row = rbase + c with c = (y+r)*66 + 16i + s
+  // fragment-read addresses: A window row = rbase + c with c = r*PW + 16i + s
   // compile-time; the swizzle bit of (rbase + c) depends only on (c & 7), so the
   // 8 residues are precomputed and c*64 becomes an immediate offset.
   const int frow = lane & 15, fpc = lane >> 4;
@@ -194,9 +206,9 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int r = tap / 3, s = tap - 3 * (tap / 3);
-      uint4 af[4], bfr[FN];
+      uint4 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < FM; ++i) {
         const int c = r * PW + i * 16 + s;
         af[i] = *reinterpret_cast<const uint4*>(Ps + apre[c & 7] + c * 64);
       }
@@ -204,7 +216,7 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
       for (int j = 0; j < FN; ++j)
         bfr[j] = *reinterpret_cast<const uint4*>(Bs + bpre + (tap * BN + j * 16) * 64);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], af[i], bfr[j]);
     }
@@ -216,7 +228,7 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
     const int img = e.img, y0 = e.y0, x0 = e.x0;
     const int n0 = e.nb * BN;
     const int oh = y0 + wave;
-    bf16* Cs = reinterpret_cast<bf16*>(smem + buf * STAGE) + wave * 64 * C::CLD;
+    bf16* Cs = reinterpret_cast<bf16*>(smem + buf * STAGE) + wave * TW * C::CLD;
     float* red = reinterpret_cast<float*>(smem + buf * STAGE + C::C_BYTES);  // [NWAVE][BN][2]
     float s1[FN], s2[FN];
 #pragma unroll
@@ -227,7 +239,7 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
       const float* U = p.border ? p.border + (size_t)n * 8 : nullptr;
       s1[j] = s2[j] = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int col = i * 16 + (lane >> 4) * 4 + r;  // pixel within the wave's row
@@ -257,24 +269,26 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
       }
     }
     __syncthreads();
-    if (stats && tid < BN) {
+    if (stats && tid < C::SG * BN) {
+      // one partial-sum row per 256 pixels: rows = M / 256 (= cnnitmo_fwd_stat_rows)
+      const int g = tid / BN, col = tid - g * BN;
+      constexpr int WPG = NWAVE / C::SG;  // waves per 256-pixel group
       float t1 = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int w = 0; w < NWAVE; ++w) {
-        t1 += red[(w * BN + tid) * 2 + 0];
-        t2 += red[(w * BN + tid) * 2 + 1];
+      for (int w = 0; w < WPG; ++w) {
+        t1 += red[((g * WPG + w) * BN + col) * 2 + 0];
+        t2 += red[((g * WPG + w) * BN + col) * 2 + 1];
       }
-      // one row per 256-pixel tile: tile index = ((img*H + y0)/4)*(W/64) + x0/64 (= m0/256)
       const long tile = ((long)img * p.ho + y0) / TH * h.tiles_x + x0 / TW;
-      float* st = p.stats + (size_t)tile * 2 * p.N;
-      st[n0 + tid] = t1;
-      st[p.N + n0 + tid] = t2;
+      float* st = p.stats + (size_t)(tile * C::SG + g) * 2 * p.N;
+      st[n0 + col] = t1;
+      st[p.N + n0 + col] = t2;
     }
-    // each wave stores its 64 pixels x BN channels as 16-byte row pieces
+    // each wave stores its TW pixels x BN channels as 16-byte row pieces
     bf16* __restrict__ O = (bf16*)p.out;
     const long mrow = ((long)img * p.ho + oh) * p.wo + x0;
 #pragma unroll
-    for (int idx = lane; idx < 64 * CPR; idx += 64) {
+    for (int idx = lane; idx < TW * CPR; idx += 64) {
       const int col = idx / CPR, cc = idx - col * CPR;
       const uint4 v = *reinterpret_cast<const uint4*>(Cs + col * C::CLD + cc * 8);
       *reinterpret_cast<uint4*>(O + (size_t)(mrow + col) * p.out_ld + p.out_off + n0 + cc * 8) = v;
@@ -282,47 +296,89 @@ __global__ __launch_bounds__(NT) void conv3x3_halo_kernel(const HaloArgs h) {
     zero_acc();
   };
 
-  // vmcnt retires in issue order: after an epilogue, the wave's CPR output stores
-  // (+2 BN-partial stores on wave 0) are younger than the loads of the next item,
-  // so the top-of-loop wait leaves exactly those in flight.
-  bool stored = false;
+  // ST-stage ring over items.  vmcnt retires in issue order and counts the
+  // epilogue's global stores too, so the wave tracks how many vector-memory ops
+  // it issued after the loads of the item it is about to consume and waits for
+  // exactly the older ones (the younger loads and stores stay in flight).  The
+  // count is a lower bound for waves whose stats stores were exec-masked off,
+  // which only makes their wait stricter.
+  constexpr int L = NPI + NBI;
+  constexpr int NST = (TW * CPR + 63) / 64;  // output store instructions per wave
+  static_assert(C::SG * BN <= 64, "BN partial sums are stored by wave 0 only");
+  const int S = NST + ((stats && wave == 0) ? 2 : 0);
   Pos ep = ip;  // position of the item being computed
-  issue(0);
-  step(ip);
+  int issued = 0;
+  int mq[ST];  // mq[k]: value of `issued` right after the loads of item t+k
+#pragma unroll
+  for (int k = 0; k < ST - 1; ++k) {
+    mq[k] = issued;
+    if (k < T) {
+      issue(k);
+      step(ip);
+      issued += L;
+      mq[k] = issued;
+    }
+  }
+  mq[ST - 1] = issued;
+  int buf = 0;  // stage of item t
   for (long t = 0; t < T; ++t) {
-    if (!stored) wait_vm<0>();
-    else if (stats && wave == 0) wait_vm<CPR + 2>();
-    else wait_vm<CPR>();
-    stored = false;
+    wait_vm_dyn(issued - mq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < T) {
-      issue((int)((t + 1) & 1));
+    if (t + ST - 1 < T) {
+      issue(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
       step(ip);
+      issued += L;
+      mq[ST - 1] = issued;
     }
-    compute((int)(t & 1));
+    compute(buf);
     if (ep.ch == nch - 1) {
       __syncthreads();  // every wave is done reading this stage: reuse it for the C tile
-      epilogue(ep, (int)(t & 1));
-      stored = true;
+      epilogue(ep, buf);
+      issued += S;
     }
     step(ep);
+#pragma unroll
+    for (int k = 0; k < ST - 1; ++k) mq[k] = mq[k + 1];
+    buf = buf == ST - 1 ? 0 : buf + 1;
   }
 }
 
-template <int BN>
-int launch_bn(const HaloArgs& h, hipStream_t s) {
-  // one workgroup per CU (LDS-limited); 256 CUs
-  hipLaunchKernelGGL((conv3x3_halo_kernel<BN>), dim3((unsigned)((h.npairs + h.per_block - 1) / h.per_block)),
-                     dim3(NT), 0, s, h);
-  return 0;
+template <int TH, int TW, int BN>
+void launch_cfg(const HaloArgs& h, hipStream_t s) {
+  // one workgroup per CU (LDS-limited); as many ring stages as fit in 160 KB
+  const dim3 grid((unsigned)((h.npairs + h.per_block - 1) / h.per_block));
+  if constexpr (3 * HaloCfg<TH, TW, BN, 1>::STAGE <= 160 * 1024)
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, TW, BN, 3>), grid, dim3(TH * 64), 0, s, h);
+  else
+    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, TW, BN, 2>), grid, dim3(TH * 64), 0, s, h);
+}
+
+int halo_cfg_env() {
+  static const int v = [] {
+    const char* e = getenv("CNNITMO_HALO_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// tile shape for a column block of BN: 0 = 4x64 (4 waves), 1 = 8x32 (8 waves), 2 = 8x64 (8 waves)
+int halo_shape(int bn) {
+  const int e = halo_cfg_env();
+  if (e >= 1 && e <= 3 && (e != 3 || bn == 32)) return e - 1;  // 8x64 exists for BN = 32 only
+  return bn == 32 ? 2 : 1;
 }
 
 }  // namespace
 
 // Applicability: bf16, 3x3 taps at stride 1, whole 4 x 64 tiles, 32-channel chunks.
 int halo_bn_for(int N) {
+  static const int force = [] {
+    const char* e = getenv("CNNITMO_HALO_BN");
+    return e ? atoi(e) : 0;
+  }();
+  if (force == 32 && N % 32 == 0) return 32;
   if (N % 64 == 0) return 64;
   if (N % 48 == 0) return 48;
   if (N % 32 == 0) return 32;
@@ -335,8 +391,12 @@ bool halo_handles(const FwdArgs& a) {
     return e ? atoi(e) : 1;
   }();
   if (!mode) return false;
+  const int bn = halo_bn_for(a.N);
+  if (bn == 0) return false;
+  const int shape = halo_shape(bn);
+  const int th = shape == 0 ? 4 : 8, tw = shape == 1 ? 32 : 64;
   return a.ntaps == 9 && a.scale == 1 && !a.scatter && a.hs == a.ho && a.ws == a.wo &&
-         a.ho % TH == 0 && a.wo % TW == 0 && a.cin % 32 == 0 && halo_bn_for(a.N) > 0 &&
+         a.ho % th == 0 && a.wo % tw == 0 && a.cin % 32 == 0 &&
          a.a_ld % 8 == 0 && a.a_off % 8 == 0 && a.out_ld % 8 == 0 && a.out_off % 8 == 0 &&
          (a.cin <= 256 || mode == 2);
 }
@@ -345,31 +405,46 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
   HaloArgs h;
   h.f = a;
   const int bn = halo_bn_for(a.N);
+  const int shape = halo_shape(bn);
+  const int th = shape == 0 ? 4 : 8, tw = shape == 1 ? 32 : 64;
   h.f.nblocks = a.N / bn;
-  h.tiles_x = a.wo / TW;
-  h.tiles_y = a.ho / TH;
+  h.tiles_x = a.wo / tw;
+  h.tiles_y = a.ho / th;
   h.nchunks = a.cin / 32;
   const long tiles = (long)a.nimg * h.tiles_x * h.tiles_y;
   h.npairs = tiles * h.f.nblocks;
   CNN_REQUIRE(h.npairs * h.nchunks < (1L << 31), "%s: too many tiles", what);
-  int cus = 256;
-  {
-    static int ncu = 0;
-    if (!ncu) {
-      int dev = 0;
-      hipDeviceProp_t prop;
-      if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-        ncu = prop.multiProcessorCount;
-      if (ncu <= 0) ncu = 256;
-    }
-    cus = ncu;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      ncu = prop.multiProcessorCount;
+    if (ncu <= 0) ncu = 256;
   }
-  h.per_block = (h.npairs + cus - 1) / cus;
+  h.per_block = (h.npairs + ncu - 1) / ncu;
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
-  switch (bn) {
-    case 64: launch_bn<64>(h, s); break;
-    case 48: launch_bn<48>(h, s); break;
-    default: launch_bn<32>(h, s); break;
+#define HC(SH, TH_, TW_)                                              \
+  if (shape == SH) {                                                  \
+    if (bn == 64) launch_cfg<TH_, TW_, 64>(h, s);                     \
+    else if (bn == 48) launch_cfg<TH_, TW_, 48>(h, s);                \
+    else launch_cfg<TH_, TW_, 32>(h, s);                              \
   }
+  HC(0, 4, 64) HC(1, 8, 32)
+#undef HC
+  if (shape == 2) launch_cfg<8, 64, 32>(h, s);
   return cnnitmo_check_launch(what);
+}
+
+const char* halo_name(const FwdArgs& a) {
+  const int bn = halo_bn_for(a.N);
+  switch (halo_shape(bn) * 100 + bn) {
+    case 64: return "conv3x3_halo_kernel<4,64,64>";
+    case 48: return "conv3x3_halo_kernel<4,64,48>";
+    case 32: return "conv3x3_halo_kernel<4,64,32>";
+    case 164: return "conv3x3_halo_kernel<8,32,64>";
+    case 148: return "conv3x3_halo_kernel<8,32,48>";
+    case 132: return "conv3x3_halo_kernel<8,32,32>";
+    default: return "conv3x3_halo_kernel<8,64,32>";
+  }
 }

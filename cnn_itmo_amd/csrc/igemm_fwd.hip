@@ -1,3 +1,4 @@
+#include <cstdio>
 // Implicit-GEMM convolution on MFMA, "forward family" (K = taps x channels).
 //
 // One kernel template serves every GEMM of the U-Net whose reduction runs over
@@ -348,6 +349,30 @@ extern "C" int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || stat_part, "conv3x3_fwd: STATS without buffer");
   CNN_REQUIRE(!(flags & CNNITMO_AFFINE) || (aff_scale && aff_shift), "conv3x3_fwd: AFFINE without coefficients");
   return dispatch(dtype, a, stream, "conv3x3_fwd");
+}
+
+// Name of the kernel cnnitmo_conv3x3_fwd (dgrad = 0) or cnnitmo_conv3x3_dgrad
+// (dgrad = 1; cin/cout as in the layer) launches for these sizes (for profiles).
+extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int w, int cin, int cout,
+                                                   int dgrad) {
+  FwdArgs a = base_args();
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = dgrad ? cout : cin;
+  a.N = dgrad ? cin : cout;
+  a.a_ld = a.cin; a.out_ld = a.N;
+  a.M = (long)n * h * w;
+  static thread_local char buf[96];
+  if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
+  const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
+  if (!use_v1() && fwd2_handles(a.N)) {
+    const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
+    snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,256x%d>", t, bn);
+  } else {
+    const Cfg c = pick_cfg(a.N);
+    snprintf(buf, sizeof(buf), "igemm_fwd_kernel<%s,%dx%d>", t, c.bm, c.bn);
+  }
+  return buf;
 }
 
 extern "C" int cnnitmo_conv1tap_fwd(int dtype, const void* cols, int k, long m, const void* wt,

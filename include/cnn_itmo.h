@@ -75,6 +75,11 @@ int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off, int n, in
                         const float* aff_shift, float* stat_part, const float* border,
                         void* stream);
 
+/* Name of the kernel conv3x3_fwd (dgrad = 0) / conv3x3_dgrad (dgrad = 1, same
+ * layer cin/cout) launches for these sizes (profiling labels; no GPU needed). */
+const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int w, int cin, int cout,
+                                        int dgrad);
+
 /* Rows of the BN partial-sum buffer written by a forward conv over m output
  * pixels with ncols GEMM columns (cout for conv3x3, 4*cout for tconv2x2). */
 int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols);

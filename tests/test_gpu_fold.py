@@ -34,7 +34,8 @@ def affine(rng, c, neg=False):
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 8, 12), (64, 128, 5, 7), (96, 64, 1, 6), (32, 64, 6, 1),
-                                          (128, 256, 3, 4), (64, 64, 8, 64), (32, 96, 4, 128)])
+                                          (128, 256, 3, 4), (64, 64, 8, 64), (32, 96, 4, 128),
+                                          (64, 64, 16, 96), (32, 32, 16, 128)])
 def test_conv3x3_folded_fwd_wgrad(dt, cin, cout, H, W):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(cin * 7 + cout + H)

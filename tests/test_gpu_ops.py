@@ -47,7 +47,8 @@ def close(got, want, dt, what=""):
 @pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 8, 12), (64, 128, 5, 7), (96, 64, 6, 10), (32, 256, 4, 4),
                                           # whole 4x64 tiles: the halo kernel (bf16) for fwd and dgrad
                                           (32, 32, 8, 64), (96, 64, 4, 128), (192, 128, 4, 64),
-                                          (64, 64, 12, 64), (32, 64, 12, 192)])
+                                          (64, 64, 12, 64), (32, 64, 12, 192), (96, 64, 16, 128),
+                                          (192, 128, 8, 64), (64, 64, 16, 64), (32, 64, 24, 192)])
 def test_conv3x3_fwd_dgrad_wgrad(dt, cin, cout, H, W):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(cin + cout)
