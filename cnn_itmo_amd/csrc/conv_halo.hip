@@ -94,7 +94,8 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
   constexpr int CPR = BN / 8;  // 16-byte output pieces per pixel
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the vmcnt switch
   const long q0 = (long)blockIdx.x * h.per_block;
   const long q1 = q0 + h.per_block < h.npairs ? q0 + h.per_block : h.npairs;
   if (q0 >= q1) return;

@@ -439,8 +439,12 @@ size_t ws_bytes_for(long P, int M, int N, int ntaps) {
 extern "C" size_t cnnitmo_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin, int cout,
                                                 int ntaps) {
   const long P = (long)n * h * w;
-  return dtype == CNNITMO_BF16 ? ws_bytes_for<bf16>(P, cout, cin, ntaps)
-                               : ws_bytes_for<float>(P, cout, cin, ntaps);
+  if (dtype == CNNITMO_BF16) {
+    size_t b = ws_bytes_for<bf16>(P, cout, cin, ntaps);
+    if (ntaps == 9) b = std::max(b, wgrad_halo_ws_bytes(n, h, w, cin, cout));
+    return b;
+  }
+  return ws_bytes_for<float>(P, cout, cin, ntaps);
 }
 
 extern "C" size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin,
@@ -480,6 +484,19 @@ extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld,
   a.tap_stride = cin; a.out_ld = ntaps * cin;
   const int cols_out = dw_cols > 0 ? dw_cols : ntaps * cin;
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == CNNITMO_BF16 && ntaps == 9) {
+    const int splits = launch_wgrad_halo((const bf16*)x, x_ld, x_off, (const bf16*)dz, n, h, w, cin, cout,
+                                         (float*)workspace, ws_bytes, s);
+    if (splits > 0) {
+      int rc = cnnitmo_check_launch("conv_wgrad");
+      if (rc) return rc;
+      const long slab = (long)cout * 9 * cin, outn = slab;
+      const int rblocks = (int)std::min<long>((outn + 255) / 256, 4096);
+      hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)workspace, slab,
+                         splits, cout, 9 * cin, cols_out, dw, f);
+      return cnnitmo_check_launch("conv_wgrad");
+    }
+  }
   if (dtype == CNNITMO_BF16)
     return run_wgrad<bf16>(a, dw, cout, ntaps * cin, cols_out, workspace, ws_bytes, s, "conv_wgrad", f);
   if (dtype == CNNITMO_F32)

@@ -1,0 +1,366 @@
+// Weight gradient of the 3x3 'same' conv for the high-resolution layers (bf16),
+// sliding-window form:
+//
+//   dW[co][t=(r,s)][ci] = sum_p dz[p][co] * x[p + (r-1, s-1)][ci]
+//
+// A workgroup owns a vertical strip of TW pixel columns, a contiguous range of
+// (image, row) rows, and a (BM output x BN input channel) block; ALL nine taps
+// of that block accumulate in registers.  Walking down the strip one row per
+// step, it loads each dz row once and each x row once (plus a 1-pixel
+// horizontal halo): the three x rows y-1, y, y+1 stay in an LDS ring and the
+// nine taps are nine (row, column-shift) windows of it.  The implicit-GEMM
+// wgrad (igemm_wgrad2.hip) instead re-gathers x for every tap; with 32..192
+// channels per pixel that re-read bounds it (dec9: 265 TFLOP/s).
+//
+// LDS images are [pixel][channel] rows filled by global_load_lds_dwordx4 and
+// read transposed with ds_read_b64_tr_b16 (K = pixels contiguous per lane); the
+// 32-byte column blocks are XOR-swizzled by row (trswz), conflict-free for
+// windows starting at any row (the column shift s; checked exhaustively, see
+// DESIGN.md).  Output: one fp32 slab [cout][9][cin] per (strip, row range),
+// reduced in a fixed order by slab_reduce_kernel (igemm_wgrad.hip), which also
+// applies the folded-BN correction.
+#include <algorithm>
+#include <cstring>
+
+#include "igemm_common.h"
+
+#pragma clang diagnostic ignored "-Winline-asm"
+
+static __device__ __attribute__((aligned(256))) unsigned char wh_zero_page[256] = {0};
+
+namespace {
+
+__device__ __forceinline__ unsigned lds_addr3(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ void glds(const void* gsrc, const char* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr3(lds));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(a) : "m0");
+}
+template <int N> __device__ __forceinline__ void waitvm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void waitvm_dyn(int n) {
+  switch (n) {
+#define W1(k) case k: waitvm<k>(); break;
+    W1(0) W1(1) W1(2) W1(3) W1(4) W1(5) W1(6) W1(7) W1(8) W1(9) W1(10) W1(11) W1(12) W1(13) W1(14) W1(15)
+    W1(16) W1(17) W1(18) W1(19) W1(20) W1(21) W1(22) W1(23) W1(24) W1(25) W1(26) W1(27) W1(28) W1(29)
+    W1(30) W1(31) W1(32) W1(33) W1(34) W1(35) W1(36) W1(37) W1(38) W1(39) W1(40) W1(41) W1(42) W1(43)
+    W1(44) W1(45) W1(46) W1(47)
+#undef W1
+    default: waitvm<0>(); break;
+  }
+}
+
+// row swizzle of the 32-byte column blocks of an R-channel bf16 row
+template <int R> __device__ __forceinline__ int trswz(int row) {
+  if constexpr (R == 32 || R == 96) return (row >> 3) & 1;
+  if constexpr (R == 64) return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+  return (row & 3) | (((row >> 3) & 1) << 2);  // R == 128
+}
+template <int R> __device__ __forceinline__ int bfo(int row, int col) {
+  return row * (R * 2) + (((col >> 4) ^ trswz<R>(row)) << 5) + ((col & 15) << 1);
+}
+
+struct WHArgs {
+  const bf16* dz;  // [P][cout]
+  int cout;
+  const bf16* x;  // view [P][x_ld] at x_off
+  long x_ld;
+  int x_off;
+  int nimg, H, W, cin;
+  float* out;  // slabs [splits][cout][9*cin]
+  long slab;
+  int strips, cbm, cbn, rsplits;
+  long rows_per;  // row steps per workgroup
+};
+
+// Waves: three groups (one per kernel row r = 0, 1, 2), each WM x WN over the
+// (BM, BN) block, so every wave keeps 3 taps x its tile in accumulators.
+template <int BM, int BN, int TW, int WM, int WN, int D>
+struct WHCfg {
+  static constexpr int NWG = WM * WN, NW = 3 * NWG, NT = NW * 64;
+  static constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16, KS = TW / 32;
+  static constexpr int XROWS = TW + 2;
+  static constexpr int XB = (XROWS * BN * 2 + 1023) / 1024;  // KB (= DMA instructions) per x row
+  static constexpr int DB = TW * BM * 2 / 1024;              // per dz row
+  static constexpr int XS = D + 3, DS = D + 1;               // ring slots
+  static constexpr int SMEM = ((XS + 1) * XB + DS * DB) * 1024;  // + one all-zero x row
+  static constexpr int LX = (XB + NW - 1) / NW, LD = (DB + NW - 1) / NW;  // max DMA per wave per row
+  static_assert(TW * BM * 2 % 1024 == 0, "dz rows must be whole KB");
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+template <int BM, int BN, int TW, int WM, int WN, int D>
+__global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHArgs p) {
+  using C = WHCfg<BM, BN, TW, WM, WN, D>;
+  constexpr int NW = C::NW, TM = C::TM, TN = C::TN, FM = C::FM, FN = C::FN, KS = C::KS;
+  constexpr int XB = C::XB, DB = C::DB, XS = C::XS, DS = C::DS, LX = C::LX, LD = C::LD;
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  char* const xbase = smem;
+  char* const zrow = smem + XS * XB * 1024;  // all-zero x row: taps across the image edge
+  char* const dbase = zrow + XB * 1024;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the vmcnt switch
+  const int wr = wave / C::NWG, wq = wave - wr * C::NWG;  // kernel row of this wave's taps
+  const int wm = wq / WN, wn = wq % WN;
+  int bid = blockIdx.x;
+  const int cb = bid % (p.cbm * p.cbn);
+  bid /= p.cbm * p.cbn;
+  const int strip = bid % p.strips;
+  const int rs = bid / p.strips;
+  const int m0 = (cb / p.cbn) * BM, n0 = (cb % p.cbn) * BN;
+  const int x0 = strip * TW;
+  const long total_rows = (long)p.nimg * p.H;
+  const long g0 = (long)rs * p.rows_per;
+  const long g1 = g0 + p.rows_per < total_rows ? g0 + p.rows_per : total_rows;
+  const int nrows = (int)(g1 - g0);
+  const int split = rs * p.strips + strip;
+
+  // ---- per-lane DMA geometry (fixed for the launch) --------------------------
+  // x row image: XROWS pixel rows (columns x0-1 .. x0+TW) of BN channels
+  int xoff[LX];  // element offset from pixel (row g, column x0)
+  bool xact[LX], xval[LX];  // lane issues this DMA / its pixel is inside the image
+#pragma unroll
+  for (int q = 0; q < LX; ++q) {
+    const int ins = wave + q * NW;
+    xact[q] = ins < XB;
+    const int off = ins * 1024 + lane * 16;
+    const int row = off / (BN * 2), pos = off - row * (BN * 2);
+    const int col = (((pos >> 5) ^ trswz<BN>(row)) << 4) + ((pos >> 4) & 1) * 8;
+    const int xx = x0 - 1 + row;
+    xval[q] = row < C::XROWS && xx >= 0 && xx < p.W;
+    xoff[q] = (int)((row - 1) * p.x_ld) + col;
+  }
+  int doff[LD];
+  bool dact[LD];
+#pragma unroll
+  for (int q = 0; q < LD; ++q) {
+    const int ins = wave + q * NW;
+    dact[q] = ins < DB;
+    const int off = ins * 1024 + lane * 16;
+    const int row = off / (BM * 2), pos = off - row * (BM * 2);
+    const int col = (((pos >> 5) ^ trswz<BM>(row)) << 4) + ((pos >> 4) & 1) * 8;
+    doff[q] = row * p.cout + col;
+  }
+  int nx = 0, nd = 0;  // DMA instructions this wave issues per x / dz row
+#pragma unroll
+  for (int q = 0; q < LX; ++q) nx += xact[q] ? 1 : 0;
+#pragma unroll
+  for (int q = 0; q < LD; ++q) nd += dact[q] ? 1 : 0;
+
+  auto issue_x = [&](long g, int slot) {
+    char* S = xbase + slot * XB * 1024;
+    const bool ok = g >= 0 && g < total_rows;
+    const bf16* base = p.x + ((size_t)g * p.W + x0) * p.x_ld + p.x_off + n0;
+#pragma unroll
+    for (int q = 0; q < LX; ++q)
+      if (xact[q]) glds(ok && xval[q] ? (const void*)(base + xoff[q]) : (const void*)wh_zero_page,
+                        S + (wave + q * NW) * 1024);
+  };
+  auto issue_d = [&](long g, int slot) {
+    char* S = dbase + slot * DB * 1024;
+    const bf16* base = p.dz + ((size_t)g * p.W + x0) * p.cout + m0;
+#pragma unroll
+    for (int q = 0; q < LD; ++q)
+      if (dact[q]) glds(base + doff[q], S + (wave + q * NW) * 1024);
+  };
+
+  f32x4 acc[3][FM][FN];  // taps (wr, s), s = 0..2
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  for (int i = tid; i < XB * 1024 / 16; i += C::NT)
+    *reinterpret_cast<uint4*>(zrow + i * 16) = uint4{0u, 0u, 0u, 0u};
+  // (ordered before the first use by the loop's barrier)
+
+  // ---- pipeline: group k = {dz row g0+k, x row g0+k+1}; x rows g0-1, g0 first --
+  int issued = 0;
+  int mq[D + 1];
+  int xslot_next = 0;  // slot for the next x row to issue (rows issued in order from g0-1)
+  int dslot_next = 0;
+  issue_x(g0 - 1, xslot_next);
+  xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+  issue_x(g0, xslot_next);
+  xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+  issued += 2 * nx;
+#pragma unroll
+  for (int k = 0; k <= D; ++k) mq[k] = issued;
+#pragma unroll
+  for (int k = 0; k < D; ++k) {
+    if (k < nrows) {
+      issue_d(g0 + k, dslot_next);
+      dslot_next = dslot_next + 1 == DS ? 0 : dslot_next + 1;
+      issue_x(g0 + k + 1, xslot_next);
+      xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+      issued += nd + nx;
+    }
+    mq[k] = issued;
+  }
+  int xs0 = 0;  // slot of x row g0+k-1
+  int ds0 = 0;  // slot of dz row g0+k
+  int y = (int)(g0 % p.H);
+  for (int k = 0; k < nrows; ++k) {
+    waitvm_dyn(issued - mq[0]);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + D < nrows) {
+      issue_d(g0 + k + D, dslot_next);
+      dslot_next = dslot_next + 1 == DS ? 0 : dslot_next + 1;
+      issue_x(g0 + k + D + 1, xslot_next);
+      xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+      issued += nd + nx;
+      mq[D] = issued;
+    }
+    // ---- compute row y: taps r = 0,1,2 read x rows y-1, y, y+1 (zero at the image edge)
+    const char* Ds = dbase + ds0 * DB * 1024;
+    const int xs1 = xs0 + 1 == XS ? 0 : xs0 + 1, xs2 = xs1 + 1 == XS ? 0 : xs1 + 1;
+    // rows outside the image read the zero row (a uniform pointer select, no branch:
+    // a skipped tap would make the compiler copy the accumulators around it)
+    const int xsr = wr == 0 ? xs0 : (wr == 1 ? xs1 : xs2);
+    const char* Xs = (wr == 0 && y == 0) || (wr == 2 && y == p.H - 1) ? zrow : xbase + xsr * XB * 1024;
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) {
+      const int r0 = kk * 32 + 8 * g + qq;
+      bf16x8 af[FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int col = wm * TM + i * 16 + 4 * pp;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + bfo<BM>(r0, col)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + bfo<BM>(r0 + 4, col)));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      {
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          bf16x8 bfr[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int col = wn * TN + j * 16 + 4 * pp;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s, col)));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s + 4, col)));
+            bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          }
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[s][i][j], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < D; ++q) mq[q] = mq[q + 1];
+    xs0 = xs1;
+    ds0 = ds0 + 1 == DS ? 0 : ds0 + 1;
+    y = y + 1 == p.H ? 0 : y + 1;
+  }
+
+  // ---- this workgroup's slab: [cout][9][cin] (its BM x BN block) ----------------
+  float* __restrict__ O = p.out + (size_t)split * p.slab;
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = m0 + wm * TM + i * 16 + g * 4 + rr;
+        const int t = wr * 3 + s;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          O[(size_t)co * 9 * p.cin + t * p.cin + n0 + wn * TN + j * 16 + li] = acc[s][i][j][rr];
+      }
+}
+
+struct WHPlan {
+  int bm, bn, tw, strips, cbm, cbn, rsplits, smem;
+  long rows_per;
+};
+
+bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
+  static const int mode = [] {
+    const char* e = getenv("CNNITMO_WGRAD_HALO");
+    return e ? atoi(e) : 1;
+  }();
+  if (!mode) return false;
+  if (cin > 192 || cout > 128) return false;  // deep layers: the implicit GEMM is not re-read bound
+  pl.bm = cout % 64 == 0 ? 64 : (cout == 32 ? 32 : 0);
+  pl.bn = cin % 96 == 0 ? 96 : (cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0));
+  if (!pl.bm || !pl.bn) return false;
+  pl.tw = (pl.bm * pl.bn <= 32 * 64 && w % 128 == 0) ? 128 : 64;
+  if (w % pl.tw) return false;
+  pl.strips = w / pl.tw;
+  pl.cbm = cout / pl.bm;
+  pl.cbn = cin / pl.bn;
+  const long rows = (long)n * h;
+  const long per = (long)pl.strips * pl.cbm * pl.cbn;
+  // whole rounds of resident workgroups: slots = CUs x workgroups per CU (LDS- or
+  // register-limited); pick the row split with the least idle tail (fewest splits on ties)
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      ncu = prop.multiProcessorCount;
+    if (ncu <= 0) ncu = 256;
+  }
+  const int xb = ((pl.tw + 2) * pl.bn * 2 + 1023) / 1024, db = pl.tw * pl.bm * 2 / 1024;
+  const int smem = (6 * xb + 3 * db) * 1024;  // D = 2
+  const int occ = std::max(1, (160 * 1024) / smem);
+  const long slots = (long)ncu * occ;
+  long best = 1;
+  double best_eff = -1.0;
+  for (long rs = 1; rs <= 64 && rs <= rows; ++rs) {
+    const long blocks = per * rs;
+    const long rounds = (blocks + slots - 1) / slots;
+    double eff = (double)blocks / (double)(rounds * slots);
+    if (blocks < slots / 2) eff *= 0.5;  // too few workgroups to fill the chip
+    if (eff > best_eff + 1e-3) { best_eff = eff; best = rs; }
+  }
+  pl.rows_per = (rows + best - 1) / best;
+  pl.rsplits = (int)((rows + pl.rows_per - 1) / pl.rows_per);
+  return true;
+}
+
+template <int BM, int BN, int TW>
+void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
+  // 12 waves (3 per SIMD) for the big blocks, 6 for the small ones
+  constexpr int WM = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1), WN = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2);
+  hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, 2>), dim3(grid), dim3(3 * WM * WN * 64), 0, s, a);
+}
+
+}  // namespace
+
+size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout) {
+  WHPlan pl;
+  if (!wh_plan(n, h, w, cin, cout, pl)) return 0;
+  return (size_t)pl.strips * pl.rsplits * cout * 9 * cin * 4;
+}
+
+// Returns the number of slabs written (>0) or -1 when this path does not apply.
+int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n, int h, int w, int cin,
+                      int cout, float* ws, size_t ws_bytes, hipStream_t s) {
+  WHPlan pl;
+  if (!wh_plan(n, h, w, cin, cout, pl)) return -1;
+  if (x_ld % 8 || x_off % 8) return -1;
+  const size_t need = (size_t)pl.strips * pl.rsplits * cout * 9 * cin * 4;
+  if (!ws || ws_bytes < need) return -1;
+  WHArgs a;
+  memset(&a, 0, sizeof(a));
+  a.dz = dz; a.cout = cout; a.x = x; a.x_ld = x_ld; a.x_off = x_off;
+  a.nimg = n; a.H = h; a.W = w; a.cin = cin;
+  a.out = ws; a.slab = (long)cout * 9 * cin;
+  a.strips = pl.strips; a.cbm = pl.cbm; a.cbn = pl.cbn; a.rsplits = pl.rsplits; a.rows_per = pl.rows_per;
+  const unsigned grid = (unsigned)(pl.strips * pl.cbm * pl.cbn * pl.rsplits);
+#define WH(BMv, BNv, TWv) \
+  if (pl.bm == BMv && pl.bn == BNv && pl.tw == TWv) { wh_launch<BMv, BNv, TWv>(a, grid, s); return pl.strips * pl.rsplits; }
+  WH(64, 96, 64) WH(64, 64, 64) WH(64, 32, 64) WH(32, 96, 64) WH(32, 64, 64) WH(32, 32, 64)
+  WH(64, 32, 128) WH(32, 64, 128) WH(32, 32, 128)
+#undef WH
+  return -1;
+}
