@@ -1,4 +1,4 @@
-// Weight gradient of the 3x3 'same' conv for the high-resolution layers (bf16),
+// Weight gradient of the 3x3 'same' conv (bf16, every U-Net 3x3 layer),
 // sliding-window form:
 //
 //   dW[co][t=(r,s)][ci] = sum_p dz[p][co] * x[p + (r-1, s-1)][ci]
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     xoff[q] = (int)((row - 1) * p.x_ld) + col;
   }
   int doff[LD];
-  bool dact[LD];
+  bool dact[LD], dval[LD];  // (the last strip may overhang the image: zero columns)
 #pragma unroll
   for (int q = 0; q < LD; ++q) {
     const int ins = wave + q * NW;
@@ -141,6 +141,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     const int row = off / (BM * 2), pos = off - row * (BM * 2);
     const int col = (((pos >> 5) ^ trswz<BM>(row)) << 4) + ((pos >> 4) & 1) * 8;
     doff[q] = row * p.cout + col;
+    dval[q] = x0 + row < p.W;
   }
   int nx = 0, nd = 0;  // DMA instructions this wave issues per x / dz row
 #pragma unroll
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     const bf16* base = p.dz + ((size_t)g * p.W + x0) * p.cout + m0;
 #pragma unroll
     for (int q = 0; q < LD; ++q)
-      if (dact[q]) glds(base + doff[q], S + (wave + q * NW) * 1024);
+      if (dact[q]) glds(dval[q] ? (const void*)(base + doff[q]) : (const void*)wh_zero_page, S + (wave + q * NW) * 1024);
   };
 
   f32x4 acc[3][FM][FN];  // taps (wr, s), s = 0..2
@@ -288,13 +289,11 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
     return e ? atoi(e) : 1;
   }();
   if (!mode) return false;
-  if (cin > 192 || cout > 128) return false;  // deep layers: the implicit GEMM is not re-read bound
   pl.bm = cout % 64 == 0 ? 64 : (cout == 32 ? 32 : 0);
   pl.bn = cin % 96 == 0 ? 96 : (cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0));
   if (!pl.bm || !pl.bn) return false;
   pl.tw = (pl.bm * pl.bn <= 32 * 64 && w % 128 == 0) ? 128 : 64;
-  if (w % pl.tw) return false;
-  pl.strips = w / pl.tw;
+  pl.strips = (w + pl.tw - 1) / pl.tw;  // a partial last strip reads zero columns
   pl.cbm = cout / pl.bm;
   pl.cbn = cin / pl.bn;
   const long rows = (long)n * h;

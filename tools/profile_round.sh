@@ -6,5 +6,5 @@ set -e
 tag=$1; shift
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$tag" -o run -- \
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_$tag" -o run -- \
   python3 "$R/bench.py" --no-cpu "$@" > "$R/gpurun_out/prof_${tag}_bench.log" 2>&1
