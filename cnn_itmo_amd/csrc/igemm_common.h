@@ -73,6 +73,7 @@ bool fwd2_handles(int N);  // v2 is the faster kernel for this column count
 bool halo_handles(const FwdArgs& a);
 int launch_halo(FwdArgs a, hipStream_t s, const char* what);
 const char* halo_name(const FwdArgs& a);
+long halo_stat_rows(const FwdArgs& a);
 
 // v2 (direct-to-LDS, multi-tap) bf16 weight gradients, igemm_wgrad2.hip
 struct Wgrad2Args {

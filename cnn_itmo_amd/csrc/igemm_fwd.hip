@@ -325,6 +325,17 @@ void set_taps3x3(FwdArgs& a) {
 
 }  // namespace
 
+// conv3x3 forward: the halo kernel writes one row per 256 pixels of each
+// (possibly partial) 8x32 / 8x64 tile, so the count depends on the frame shape.
+extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int cin, int cout) {
+  FwdArgs a = base_args();
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cin; a.N = cout; a.a_ld = cin; a.out_ld = cout; a.M = (long)n * h * w;
+  if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_stat_rows(a);
+  return cnnitmo_fwd_stat_rows(dtype, a.M, cout);
+}
+
 extern "C" int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols) {
   (void)dtype;
   if (!use_v1() && fwd2_handles(ncols)) return fwd2_stat_rows(m);

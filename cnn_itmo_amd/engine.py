@@ -227,7 +227,10 @@ class BlockStage(Stage):
             self._conv(n, out, (L.RELU if self.relu else 0) | L.AFFINE, aff=(sc, sh))
             return
         m, ncols = self._gemm_rows(n)
-        rows = ops.fwd_stat_rows(e.dt, m, ncols)
+        if self.kind == "c3":
+            rows = ops.conv3x3_stat_rows(e.dt, n, self.vout.h, self.vout.w, self.cin, cout)
+        else:
+            rows = ops.fwd_stat_rows(e.dt, m, ncols)
         stats = torch.empty(rows * 2 * ncols, device=e.device, dtype=torch.float32)
         if self.vout.folded:  # r goes straight into the output (slice); consumers fold the BN
             rview = out

@@ -76,6 +76,10 @@ def fwd_stat_rows(dt, m, ncols):
     return query("cnnitmo_fwd_stat_rows", dt, m, ncols)
 
 
+def conv3x3_stat_rows(dt, n, h, w, cin, cout):
+    return query("cnnitmo_conv3x3_stat_rows", dt, n, h, w, cin, cout)
+
+
 def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx: View):
     call("cnnitmo_conv3x3_dgrad", dt, ptr(dz), n, h, w, cout, ptr(wflip), cin, dx.ptr, dx.ld, dx.off,
          stream_ptr())

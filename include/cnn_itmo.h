@@ -81,8 +81,10 @@ const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int w, int cin,
                                         int dgrad);
 
 /* Rows of the BN partial-sum buffer written by a forward conv over m output
- * pixels with ncols GEMM columns (cout for conv3x3, 4*cout for tconv2x2). */
+ * pixels with ncols GEMM columns (4*cout for tconv2x2; the 1-tap first layer).
+ * conv3x3: use cnnitmo_conv3x3_stat_rows (the row count depends on the frame). */
 int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols);
+long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int cin, int cout);
 
 /* Input-gradient of conv3x3 (TF Conv2DBackpropInput).  dz: [n,h,w,cout]
  * contiguous; wt_flip: [cin][3][3][cout] = W[co][2-r][2-s][ci] (from

@@ -53,7 +53,7 @@ def test_conv3x3_folded_fwd_wgrad(dt, cin, cout, H, W):
     ops.fold_conv3x3(d, cu(w), cu(b), cu(s), cu(h), cout, cin, wout, bout, border)
     rv = ops.View(dev(rb, dt).reshape(-1), N, H, W, cin, ld, off)
     out = ops.new_view(N, H, W, cout, TDT[dt])
-    rows = ops.fwd_stat_rows(d, N * H * W, cout)
+    rows = ops.conv3x3_stat_rows(d, N, H, W, cin, cout)
     stats = torch.zeros(rows, 2, cout, device="cuda")
     ops.conv3x3_fwd(d, rv, wout, bout, out, flags=1 | 2, stats=stats, border=border)
     torch.cuda.synchronize()

@@ -69,7 +69,7 @@ def test_conv3x3_fwd_dgrad_wgrad(dt, cin, cout, H, W):
     wflip = torch.empty(w.size, dtype=TDT[dt], device="cuda")
     ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cin, wf, wflip)
     out = ops.new_view(N, H, W, cout, TDT[dt])
-    rows = ops.fwd_stat_rows(d, N * H * W, cout)
+    rows = ops.conv3x3_stat_rows(d, N, H, W, cin, cout)
     stats = torch.zeros(rows, 2, cout, device="cuda")
     ops.conv3x3_fwd(d, xv, wf, torch.tensor(b).cuda(), out, flags=1 | 2, stats=stats)
     torch.cuda.synchronize()
