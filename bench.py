@@ -114,16 +114,18 @@ class KernelTimer:
             fl = 2.0 * m * out.c * 27  # algorithmic K = 3x3x3 (the packed 32 has 5 zero columns)
             return self._bracket(self.fwd_name(dt, out.c), fl, o["conv1tap_fwd"], dt, cols, kk, m, wt, bias, out, *a, **k)
 
+        def wname(dt, ntaps, n, h, w, cin, cout):
+            k = ops.query("cnnitmo_wgrad_kernel_name", dt, ntaps, n, h, w, cin, cout).decode()
+            return k + " + slab_reduce"
+
         def conv_wgrad(dt, ntaps, x, dz, cout, dw, dw_cols=0, fold=None):
             fl = 2.0 * x.p * cout * (27 if ntaps == 1 else 9 * x.c)
-            t = "bf16" if dt == 1 else "f32"
-            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad2_kernel + slab_reduce)", fl, o["conv_wgrad"],
+            return self._bracket(wname(dt, ntaps, x.n, x.h, x.w, x.c, cout), fl, o["conv_wgrad"],
                                  dt, ntaps, x, dz, cout, dw, dw_cols, fold)
 
         def tconv_wgrad(dt, x, dout, cout, dk, fold=None):
             fl = 2.0 * x.p * 4 * cout * x.c
-            t = "bf16" if dt == 1 else "f32"
-            return self._bracket(f"conv_wgrad[{t}] (igemm_wgrad2_kernel + slab_reduce)", fl, o["tconv_wgrad"],
+            return self._bracket(wname(dt, 4, x.n, x.h, x.w, x.c, cout), fl, o["tconv_wgrad"],
                                  dt, x, dout, cout, dk, fold)
 
         for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad), ("tconv_fwd", tconv_fwd),
@@ -256,7 +258,9 @@ def main():
     pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get(name, {}).get("bytes_per_launch")
+            tab = json.load(open(pmc))
+            key = name.split(" + ")[0]  # wgrad ops: the main kernel (slab_reduce excluded)
+            traffic = tab.get(key, {}).get("bytes_per_launch")
         except Exception:
             traffic = None
     roof = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

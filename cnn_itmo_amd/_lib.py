@@ -68,6 +68,7 @@ SIGNATURES = {
     "cnnitmo_border_rows": (i32, [i32]),
     "cnnitmo_conv3x3_stat_rows": (i64, [i32, i32, i32, i32, i32, i32]),
     "cnnitmo_conv3x3_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
+    "cnnitmo_wgrad_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_border_sums": (i32, [i32, vp, i32, i32, i32, i32, vp, vp]),
     "cnnitmo_rmsprop": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, vp]),
 }

@@ -96,9 +96,15 @@ struct Wgrad2Args {
 };
 
 int launch_wgrad2(Wgrad2Args a, void* ws, size_t ws_bytes, hipStream_t s);
+struct W2Label {
+  bool ok;
+  int bm, bn, tpb;
+};
+W2Label wgrad2_label(long P, int M, int N, int ntaps);
 size_t wgrad2_ws_bytes(long P, int M, int N, int ntaps);
 
 // sliding-window bf16 3x3 weight gradient for the high-resolution layers, wgrad_halo.hip
 size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout);
+const char* wgrad_halo_name(int n, int h, int w, int cin, int cout);
 int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n, int h, int w, int cin,
                       int cout, float* ws, size_t ws_bytes, hipStream_t s);

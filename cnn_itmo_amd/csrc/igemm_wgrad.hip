@@ -1,3 +1,4 @@
+#include <cstdio>
 // Implicit-GEMM weight gradients on MFMA (K = pixels).
 //
 //   conv3x3 wgrad  (TF Conv2DBackpropFilter for model.py:196):
@@ -535,4 +536,27 @@ extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout
     return run_wgrad<float>(a, dk, 4 * cout, cin, cin, workspace, ws_bytes, s, "tconv2x2_wgrad", f);
   cnnitmo_set_error("tconv2x2_wgrad: unsupported dtype %d", dtype);
   return CNNITMO_EUNSUPPORTED;
+}
+
+// Label of the main kernel cnnitmo_conv_wgrad (ntaps 9 / 1) or
+// cnnitmo_tconv2x2_wgrad (ntaps 4) launches for these sizes (for profiles;
+// each is followed by slab_reduce_kernel).
+extern "C" const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, int h, int w, int cin,
+                                                 int cout) {
+  if (dtype == CNNITMO_BF16 && ntaps == 9) {
+    const char* hn = wgrad_halo_name(n, h, w, cin, cout);
+    if (hn[0]) return hn;
+  }
+  const long P = (long)n * h * w;
+  static thread_local char buf[80];
+  if (dtype == CNNITMO_BF16 && !wgrad_v1()) {
+    const W2Label l = wgrad2_label(P, cout, cin, ntaps);
+    if (l.ok) {
+      snprintf(buf, sizeof(buf), "igemm_wgrad2_kernel<%d,%d,tpb%d>", l.bm, l.bn, l.tpb);
+      return buf;
+    }
+  }
+  const int bm = pick_tile(cout), bn = pick_tile(cin);
+  snprintf(buf, sizeof(buf), "igemm_wgrad_kernel<%s,%d,%d>", dtype == CNNITMO_BF16 ? "bf16" : "f32", bm, bn);
+  return buf;
 }

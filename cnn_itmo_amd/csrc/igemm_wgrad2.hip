@@ -280,10 +280,12 @@ static void w2_launch(const Wgrad2Args& a, hipStream_t s, unsigned grid) {
 }
 
 // conv3x3 (DEP 0): taps per block 1 / 3 / 9; tconv (DEP 1): 1 / 2 / 4.
-static bool w2_dispatch(const Wgrad2Args& a, const W2Plan& pl, hipStream_t s, unsigned grid, int dep) {
+// dry_run: only report whether the plan is one of the instantiated kernels
+static bool w2_dispatch(const Wgrad2Args& a, const W2Plan& pl, hipStream_t s, unsigned grid, int dep,
+                        bool dry_run = false) {
 #define W2(BMv, BNv, WMv, WNv, TPBv, DEPv)                                     \
   if (pl.bm == BMv && pl.bn == BNv && pl.tpb == TPBv && dep == DEPv) {        \
-    w2_launch<BMv, BNv, WMv, WNv, TPBv, DEPv>(a, s, grid);                    \
+    if (!dry_run) w2_launch<BMv, BNv, WMv, WNv, TPBv, DEPv>(a, s, grid);      \
     return true;                                                              \
   }
   // reachable (tile, taps-per-block) plans of w2_tiles; anything else falls back to
@@ -315,4 +317,13 @@ int launch_wgrad2(Wgrad2Args a, void* ws, size_t ws_bytes, hipStream_t s) {
   a.pix_per_split = pl.pps;
   const long total = (long)pl.mblocks * pl.nblocks * pl.tgroups * pl.splits;
   return w2_dispatch(a, pl, s, (unsigned)total, a.a_tapdep) ? pl.splits : -2;
+}
+
+W2Label wgrad2_label(long P, int M, int N, int ntaps) {
+  const W2Plan pl = w2_plan(P, M, N, ntaps);
+  W2Label l{false, pl.bm, pl.bn, pl.tpb};
+  Wgrad2Args a;
+  memset(&a, 0, sizeof(a));
+  l.ok = w2_dispatch(a, pl, nullptr, 0, ntaps == 4 ? 1 : 0, true);
+  return l;
 }

@@ -20,6 +20,7 @@
 // reduced in a fixed order by slab_reduce_kernel (igemm_wgrad.hip), which also
 // applies the folded-BN correction.
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include "igemm_common.h"
@@ -362,4 +363,13 @@ int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n
   WH(64, 32, 128) WH(32, 64, 128) WH(32, 32, 128)
 #undef WH
   return -1;
+}
+
+// kernel label for profiles ("" when this path does not apply)
+const char* wgrad_halo_name(int n, int h, int w, int cin, int cout) {
+  WHPlan pl;
+  if (!wh_plan(n, h, w, cin, cout, pl)) return "";
+  static thread_local char buf[64];
+  snprintf(buf, sizeof(buf), "wgrad_halo_kernel<%d,%d,%d>", pl.bm, pl.bn, pl.tw);
+  return buf;
 }

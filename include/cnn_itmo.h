@@ -98,6 +98,9 @@ int cnnitmo_conv3x3_dgrad(int dtype, const void* dz, int n, int h, int w, int co
  * ntaps = 9 for the 3x3 conv, 1 for a 1x1 / pre-packed (im2col) input. */
 size_t cnnitmo_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin, int cout,
                                      int ntaps);
+/* Label of the main kernel a weight gradient launches for these sizes (ntaps 9 /
+ * 1: conv, 4: tconv2x2; profiling only, no GPU needed). */
+const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, int h, int w, int cin, int cout);
 int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
                        const void* dz, int n, int h, int w, int cin, int cout, float* dw,
                        int dw_cols, const float* fold_scale, const float* fold_shift,
