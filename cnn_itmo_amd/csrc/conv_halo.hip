@@ -12,8 +12,8 @@
 //   B fragment (tap t; 16 output channels) = wstage rows t*BN + j*16 .. +15
 // LDS rows are 64 B (32 bf16); piece c of row q is stored at piece
 // c ^ (((q >> 2) & 1) << 1), which keeps every ds_read_b128 lane group
-// conflict-free for windows starting at ANY row (tools: brute-force check in
-// DESIGN.md).  Operands arrive by global_load_lds_dwordx4 (lane-linear LDS
+// conflict-free for windows starting at ANY row (exhaustive check:
+// tools/check_swizzle.py).  Operands arrive by global_load_lds_dwordx4 (lane-linear LDS
 // image, swizzle applied to the source piece).
 //
 // Persistent grid: one workgroup per CU walks a contiguous range of

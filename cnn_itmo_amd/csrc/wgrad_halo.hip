@@ -15,8 +15,7 @@
 // LDS images are [pixel][channel] rows filled by global_load_lds_dwordx4 and
 // read transposed with ds_read_b64_tr_b16 (K = pixels contiguous per lane); the
 // 32-byte column blocks are XOR-swizzled by row (trswz), conflict-free for
-// windows starting at any row (the column shift s; checked exhaustively, see
-// DESIGN.md).  Output: one fp32 slab [cout][9][cin] per (strip, row range),
+// windows starting at any row (the column shift s; tools/check_swizzle.py).  Output: one fp32 slab [cout][9][cin] per (strip, row range),
 // reduced in a fixed order by slab_reduce_kernel (igemm_wgrad.hip), which also
 // applies the folded-BN correction.
 #include <algorithm>

@@ -148,3 +148,11 @@ def test_keras_weight_layout_roundtrip():
     m.set_weights(ws)
     for a, b in zip(ws, m.get_weights()):
         assert np.array_equal(a, b)
+
+
+def test_lds_swizzles_conflict_free():
+    """The halo kernels' XOR swizzles are bank-conflict-free for windows at any row."""
+    import tools.check_swizzle as cs
+    assert cs.check_b128()
+    for R in (32, 64, 96, 128):
+        assert cs.check_tr(R), R
