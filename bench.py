@@ -102,13 +102,18 @@ class KernelTimer:
             return self._bracket(kname(dt, n, h, w, cin, cout, 1), fl, o["conv3x3_dgrad"], dt, dz, n, h, w, cout,
                                  wflip, cin, dx)
 
+        def tname(dt, n, h, w, cin, cout, dgrad):
+            return ops.query("cnnitmo_tconv2x2_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
+
         def tconv_fwd(dt, x, k_, bias, out, *a, **k):
             fl = 2.0 * x.p * 4 * out.c * x.c
-            return self._bracket(self.fwd_name(dt, 4 * out.c), fl, o["tconv_fwd"], dt, x, k_, bias, out, *a, **k)
+            return self._bracket(tname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, o["tconv_fwd"], dt, x, k_, bias, out,
+                                 *a, **k)
 
         def tconv_dgrad(dt, dout, n, h, w, cout, kT, cin, dx):
             fl = 2.0 * n * h * w * cin * 4 * cout
-            return self._bracket(self.fwd_name(dt, cin), fl, o["tconv_dgrad"], dt, dout, n, h, w, cout, kT, cin, dx)
+            return self._bracket(tname(dt, n, h, w, cin, cout, 1), fl, o["tconv_dgrad"], dt, dout, n, h, w, cout,
+                                 kT, cin, dx)
 
         def conv1tap_fwd(dt, cols, kk, m, wt, bias, out, *a, **k):
             fl = 2.0 * m * out.c * 27  # algorithmic K = 3x3x3 (the packed 32 has 5 zero columns)

@@ -67,8 +67,10 @@ SIGNATURES = {
     "cnnitmo_fold_tconv2x2": (i32, [i32, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
     "cnnitmo_border_rows": (i32, [i32]),
     "cnnitmo_conv3x3_stat_rows": (i64, [i32, i32, i32, i32, i32, i32]),
+    "cnnitmo_tconv2x2_stat_rows": (i64, [i32, i32, i32, i32, i32, i32]),
     "cnnitmo_conv3x3_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_wgrad_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
+    "cnnitmo_tconv2x2_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_border_sums": (i32, [i32, vp, i32, i32, i32, i32, vp, vp]),
     "cnnitmo_rmsprop": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, vp]),
 }

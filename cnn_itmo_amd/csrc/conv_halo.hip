@@ -23,6 +23,8 @@
 // (bias, ReLU, inference BN affine, folded-BN border correction, BN partial
 // sums: the same semantics as igemm_fwd2) stages each wave's 64 x BN tile in
 // the stage it just consumed and stores 16-byte rows.
+#include <cstdio>
+
 #include "igemm_common.h"
 
 namespace {
@@ -60,26 +62,32 @@ __device__ __forceinline__ int hswz(int row, int piece) {
   return (row << 6) + ((piece ^ (((row >> 2) & 1) << 1)) << 4);
 }
 
-// Tile TH x TW output pixels, one wave per output row (FM = TW/16 fragments),
-// BN output channels per item, ST-deep LDS ring.
-template <int TH, int TW, int BN, int ST>
+// Tile TH x TW GEMM-row pixels, one wave per tile row (FM = TW/16 fragments),
+// BN output columns per item, ST-deep LDS ring.
+//   MODE 0: conv3x3 'same' (9 taps, (TH+2) x (TW+2) halo patch)
+//   MODE 1: Conv2DTranspose(2, s2) forward: a 1x1 GEMM over the input pixels
+//           (TH x TW patch, no halo) whose column n = tap*cout + co is scattered
+//           to output pixel (2y + tap/2, 2x + tap%2)
+template <int MODE, int TH, int TW, int BN, int ST>
 struct HaloCfg {
   static constexpr int NWAVE = TH, NT = NWAVE * 64;
   static constexpr int FM = TW / 16, FN = BN / 16;
-  static constexpr int PW = TW + 2, PROWS = (TH + 2) * PW;
+  static constexpr int KT = MODE == 0 ? 9 : 1;  // taps
+  static constexpr int PW = MODE == 0 ? TW + 2 : TW, PROWS = (MODE == 0 ? TH + 2 : TH) * PW;
   static constexpr int P_INSTR = ((PROWS + 15) / 16 + NWAVE - 1) / NWAVE * NWAVE;
-  static constexpr int B_ROWS = 9 * BN;
+  static constexpr int B_ROWS = KT * BN;
   static constexpr int B_INSTR = ((B_ROWS + 15) / 16 + NWAVE - 1) / NWAVE * NWAVE;
   static constexpr int NPI = P_INSTR / NWAVE, NBI = B_INSTR / NWAVE;
   static constexpr int PATCH = P_INSTR * 1024;
   static constexpr int STAGE = PATCH + B_INSTR * 1024;
   static constexpr int CLD = BN + 8;  // C staging row (bf16), per wave TW rows
   static constexpr int C_BYTES = NWAVE * TW * CLD * 2;
-  static constexpr int SMEM = ST * STAGE;
+  // the epilogue stages C in the stage it just consumed when it fits, else in its own region
+  static constexpr bool C_IN_STAGE = C_BYTES + NWAVE * BN * 8 <= STAGE;
+  static constexpr int C_OFF = ST * STAGE;
+  static constexpr int SMEM = ST * STAGE + (C_IN_STAGE ? 0 : C_BYTES + NWAVE * BN * 8);
   static constexpr int SG = TH * TW / 256;  // BN-partial-sum rows per tile (256 pixels each)
   static_assert(TH * TW % 256 == 0 && TW % 16 == 0, "tile");
-  static_assert(C_BYTES + NWAVE * BN * 8 <= STAGE, "epilogue staging must fit in one stage");
-  static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
 struct HaloArgs {
@@ -90,9 +98,11 @@ struct HaloArgs {
   int nchunks;           // cin / 32
 };
 
-template <int TH, int TW, int BN, int ST>
-__global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h) {
-  using C = HaloCfg<TH, TW, BN, ST>;
+template <int MODE, int TH, int TW, int BN, int ST>
+__global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
+  using C = HaloCfg<MODE, TH, TW, BN, ST>;
+  constexpr int KT = C::KT;
+  static_assert(C::SMEM <= 160 * 1024, "LDS");
   constexpr int NWAVE = C::NWAVE, FM = C::FM, FN = C::FN, STAGE = C::STAGE, PW = C::PW;
   constexpr int NPI = C::NPI, NBI = C::NBI;
   constexpr int CPR = BN / 8;  // 16-byte output pieces per pixel
@@ -107,7 +117,7 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
   const long T = (q1 - q0) * nch;
   const bf16* __restrict__ X = (const bf16*)p.a;
   const bf16* __restrict__ Wt = (const bf16*)p.b;
-  const int K = 9 * p.cin;
+  const int K = KT * p.cin;
   const int tpi = h.tiles_x * h.tiles_y;
 
   // position of an item: (img, tile row, tile column, column block, chunk);
@@ -151,9 +161,10 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
     const int row = (wave * NPI + i) * 16 + lrow;
     const int piece = lpc ^ (((row >> 2) & 1) << 1);
     const int py = row / PW, px = row - (row / PW) * PW;
-    ppy[i] = row < C::PROWS ? py : -(1 << 29);  // padded rows: never in bounds, never loaded
-    ppx[i] = px;
-    poff[i] = ((long)(py - 1) * p.ws + (px - 1)) * p.a_ld + piece * 8;
+    const int dy = MODE == 0 ? py - 1 : py, dx = MODE == 0 ? px - 1 : px;  // source offset from the tile origin
+    ppy[i] = row < C::PROWS ? dy : -(1 << 29);  // padded rows: never in bounds, never loaded
+    ppx[i] = dx;
+    poff[i] = ((long)dy * p.ws + dx) * p.a_ld + piece * 8;
   }
   int boff[NBI];
 #pragma unroll
@@ -169,14 +180,15 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
     char* Ps = smem + buf * STAGE;
     char* Bs = Ps + C::PATCH;
     const bf16* tb = X + ((size_t)((long)s.img * p.hs + s.y0) * p.ws + s.x0) * p.a_ld + p.a_off + s.ch * 32;
-    const bool interior = s.y0 >= 1 && s.y0 + TH < p.hs && s.x0 >= 1 && s.x0 + TW < p.ws;
+    constexpr int lo = MODE == 0 ? 1 : 0;  // halo reach above / left of the tile
+    const bool interior = s.y0 >= lo && s.y0 + TH + lo <= p.hs && s.x0 >= lo && s.x0 + TW + lo <= p.ws;
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
       const void* src = h_zero_page;
       if (interior) {
-        if (ppy[i] >= 0) src = tb + poff[i];
+        if (ppy[i] > -(1 << 28)) src = tb + poff[i];
       } else {
-        const int yy = s.y0 + ppy[i] - 1, xx = s.x0 + ppx[i] - 1;
+        const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
         if ((unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws) src = tb + poff[i];
       }
       glds16(src, Ps + (wave * NPI + i) * 1024);
@@ -209,8 +221,8 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
     const char* Ps = smem + buf * STAGE;
     const char* Bs = Ps + C::PATCH;
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int r = tap / 3, s = tap - 3 * (tap / 3);
+    for (int tap = 0; tap < KT; ++tap) {
+      const int r = MODE == 0 ? tap / 3 : 0, s = MODE == 0 ? tap - 3 * (tap / 3) : 0;
       uint4 af[FM], bfr[FN];
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -234,14 +246,18 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
     const int n0 = e.nb * BN;
     const int oh = y0 + wave;
     const bool rowok = oh < p.ho;
-    bf16* Cs = reinterpret_cast<bf16*>(smem + buf * STAGE) + wave * TW * C::CLD;
-    float* red = reinterpret_cast<float*>(smem + buf * STAGE + C::C_BYTES);  // [NWAVE][BN][2]
+    char* cbase = C::C_IN_STAGE ? smem + buf * STAGE : smem + C::C_OFF;
+    bf16* Cs = reinterpret_cast<bf16*>(cbase) + wave * TW * C::CLD;
+    float* red = reinterpret_cast<float*>(cbase + C::C_BYTES);  // [NWAVE][BN][2]
+    // MODE 1: this column block is one tap of the tconv (BN divides cout)
+    const int tap1 = MODE == 1 ? n0 / p.cout : 0, co0 = MODE == 1 ? n0 - tap1 * p.cout : n0;
     float s1[FN], s2[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + j * 16 + (lane & 15);
-      const float bj = p.bias ? p.bias[n] : 0.f;
-      const float sj = aff ? p.aff_scale[n] : 1.f, hj = aff ? p.aff_shift[n] : 0.f;
+      const int co = MODE == 1 ? co0 + j * 16 + (lane & 15) : n;
+      const float bj = p.bias ? p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : co] : 0.f;
+      const float sj = aff ? p.aff_scale[co] : 1.f, hj = aff ? p.aff_shift[co] : 0.f;
       const float* U = p.border ? p.border + (size_t)n * 8 : nullptr;
       s1[j] = s2[j] = 0.f;
 #pragma unroll
@@ -293,13 +309,16 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
     }
     // each wave stores its TW pixels x BN channels as 16-byte row pieces
     bf16* __restrict__ O = (bf16*)p.out;
-    const long mrow = ((long)img * p.ho + oh) * p.wo + x0;
+    // MODE 0: output pixel (oh, x0 + col); MODE 1: (2*oh + tap/2, 2*(x0 + col) + tap%2) of the 2x grid
+    const long mrow = MODE == 0 ? ((long)img * p.ho + oh) * p.wo + x0
+                                : ((long)img * 2 * p.ho + 2 * oh + (tap1 >> 1)) * 2 * p.wo + 2 * x0 + (tap1 & 1);
+    constexpr int PSTEP = MODE == 0 ? 1 : 2;  // output pixels per GEMM row step
 #pragma unroll
     for (int idx = lane; idx < TW * CPR; idx += 64) {
       const int col = idx / CPR, cc = idx - col * CPR;
       const uint4 v = *reinterpret_cast<const uint4*>(Cs + col * C::CLD + cc * 8);
       uint4* dst = (rowok && x0 + col < p.wo)
-                       ? reinterpret_cast<uint4*>(O + (size_t)(mrow + col) * p.out_ld + p.out_off + n0 + cc * 8)
+                       ? reinterpret_cast<uint4*>(O + (size_t)(mrow + PSTEP * col) * p.out_ld + p.out_off + co0 + cc * 8)
                        : h_sink + lane;
       *dst = v;
     }
@@ -314,8 +333,8 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
   // which only makes their wait stricter.
   constexpr int L = NPI + NBI;
   constexpr int NST = (TW * CPR + 63) / 64;  // output store instructions per wave
-  static_assert(C::SG * BN <= 64, "BN partial sums are stored by wave 0 only");
-  const int S = NST + ((stats && wave == 0) ? 2 : 0);
+  // BN partial sums are stored by threads tid < SG*BN: waves 0 .. (SG*BN-1)/64
+  const int S = NST + ((stats && wave * 64 < C::SG * BN) ? 2 : 0);
   Pos ep = ip;  // position of the item being computed
   int issued = 0;
   int mq[ST];  // mq[k]: value of `issued` right after the loads of item t+k
@@ -355,14 +374,16 @@ __global__ __launch_bounds__(TH * 64) void conv3x3_halo_kernel(const HaloArgs h)
   }
 }
 
-template <int TH, int TW, int BN>
+template <int MODE, int TH, int TW, int BN>
 void launch_cfg(const HaloArgs& h, hipStream_t s) {
   // one workgroup per CU (LDS-limited); as many ring stages as fit in 160 KB
   const dim3 grid((unsigned)((h.npairs + h.per_block - 1) / h.per_block));
-  if constexpr (3 * HaloCfg<TH, TW, BN, 1>::STAGE <= 160 * 1024)
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, TW, BN, 3>), grid, dim3(TH * 64), 0, s, h);
+  if constexpr (HaloCfg<MODE, TH, TW, BN, 5>::SMEM <= 160 * 1024)
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 5>), grid, dim3(TH * 64), 0, s, h);
+  else if constexpr (HaloCfg<MODE, TH, TW, BN, 3>::SMEM <= 160 * 1024)
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 3>), grid, dim3(TH * 64), 0, s, h);
   else
-    hipLaunchKernelGGL((conv3x3_halo_kernel<TH, TW, BN, 2>), grid, dim3(TH * 64), 0, s, h);
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 2>), grid, dim3(TH * 64), 0, s, h);
 }
 
 int halo_cfg_env() {
@@ -373,53 +394,61 @@ int halo_cfg_env() {
   return v;
 }
 
-// tile shape for a column block of BN: 0 = 4x64 (4 waves), 1 = 8x32 (8 waves), 2 = 8x64 (8 waves)
-int halo_shape(int bn) {
-  const int e = halo_cfg_env();
-  if (e >= 1 && e <= 3 && (e != 3 || bn == 32)) return e - 1;  // 8x64 exists for BN = 32 only
-  return bn == 32 ? 2 : 1;
+struct HaloPlan {
+  int mode, bn, th, tw;
+};
+
+// mode 0: conv3x3 stride 1 ('same'); mode 1: tconv2x2 s2 forward (pixel scatter)
+bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
+  static const int en = [] {
+    const char* e = getenv("CNNITMO_HALO");
+    return e ? atoi(e) : 1;
+  }();
+  if (!en) return false;
+  if (a.cin % 32 || a.a_ld % 8 || a.a_off % 8 || a.out_ld % 8 || a.out_off % 8) return false;
+  if (a.ntaps == 9 && a.scale == 1 && !a.scatter && a.hs == a.ho && a.ws == a.wo) {
+    pl.mode = 0;
+    static const int force = [] {
+      const char* e = getenv("CNNITMO_HALO_BN");
+      return e ? atoi(e) : 0;
+    }();
+    if (force == 32 && a.N % 32 == 0) pl.bn = 32;
+    else pl.bn = a.N % 64 == 0 ? 64 : (a.N % 48 == 0 ? 48 : (a.N % 32 == 0 ? 32 : 0));
+    if (!pl.bn) return false;
+    // tile: 0 = 4x64 (4 waves), 1 = 8x32 (8 waves), 2 = 8x64 (8 waves, BN = 32 only)
+    const int e = halo_cfg_env();
+    int shape = pl.bn == 32 ? 2 : 1;
+    if (e >= 1 && e <= 3 && (e != 3 || pl.bn == 32)) shape = e - 1;
+    pl.th = shape == 0 ? 4 : 8;
+    pl.tw = shape == 1 ? 32 : 64;
+    return true;
+  }
+  if (a.ntaps == 1 && a.scale == 1 && a.scatter && a.hs == a.ho && a.ws == a.wo && a.cout % 64 == 0 &&
+      a.N == 4 * a.cout) {
+    pl.mode = 1;
+    pl.bn = a.cout % 128 == 0 ? 128 : 64;  // a column block never straddles two taps
+    pl.th = 8;
+    pl.tw = 32;
+    return true;
+  }
+  return false;
 }
 
 }  // namespace
 
-// Applicability: bf16, 3x3 taps at stride 1, whole 4 x 64 tiles, 32-channel chunks.
-int halo_bn_for(int N) {
-  static const int force = [] {
-    const char* e = getenv("CNNITMO_HALO_BN");
-    return e ? atoi(e) : 0;
-  }();
-  if (force == 32 && N % 32 == 0) return 32;
-  if (N % 64 == 0) return 64;
-  if (N % 48 == 0) return 48;
-  if (N % 32 == 0) return 32;
-  return 0;
-}
-
 bool halo_handles(const FwdArgs& a) {
-  static const int mode = [] {
-    const char* e = getenv("CNNITMO_HALO");
-    return e ? atoi(e) : 1;
-  }();
-  if (!mode) return false;
-  const int bn = halo_bn_for(a.N);
-  if (bn == 0) return false;
-  const int shape = halo_shape(bn);
-  const int th = shape == 0 ? 4 : 8, tw = shape == 1 ? 32 : 64;
-  (void)th;
-  (void)tw;
-  return a.ntaps == 9 && a.scale == 1 && !a.scatter && a.hs == a.ho && a.ws == a.wo && a.cin % 32 == 0 &&
-         a.a_ld % 8 == 0 && a.a_off % 8 == 0 && a.out_ld % 8 == 0 && a.out_off % 8 == 0;
+  HaloPlan pl;
+  return halo_plan(a, pl);
 }
 
 int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
+  HaloPlan pl;
+  CNN_REQUIRE(halo_plan(a, pl), "%s: no halo plan", what);
   HaloArgs h;
   h.f = a;
-  const int bn = halo_bn_for(a.N);
-  const int shape = halo_shape(bn);
-  const int th = shape == 0 ? 4 : 8, tw = shape == 1 ? 32 : 64;
-  h.f.nblocks = a.N / bn;
-  h.tiles_x = (a.wo + tw - 1) / tw;  // partial edge tiles are masked
-  h.tiles_y = (a.ho + th - 1) / th;
+  h.f.nblocks = a.N / pl.bn;
+  h.tiles_x = (a.wo + pl.tw - 1) / pl.tw;  // partial edge tiles are masked
+  h.tiles_y = (a.ho + pl.th - 1) / pl.th;
   h.nchunks = a.cin / 32;
   const long tiles = (long)a.nimg * h.tiles_x * h.tiles_y;
   h.npairs = tiles * h.f.nblocks;
@@ -434,37 +463,36 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
   }
   h.per_block = (h.npairs + ncu - 1) / ncu;
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
-#define HC(SH, TH_, TW_)                                              \
-  if (shape == SH) {                                                  \
-    if (bn == 64) launch_cfg<TH_, TW_, 64>(h, s);                     \
-    else if (bn == 48) launch_cfg<TH_, TW_, 48>(h, s);                \
-    else launch_cfg<TH_, TW_, 32>(h, s);                              \
+  if (pl.mode == 1) {
+    if (pl.bn == 128) launch_cfg<1, 8, 32, 128>(h, s);
+    else launch_cfg<1, 8, 32, 64>(h, s);
+  } else if (pl.th == 4) {
+    if (pl.bn == 64) launch_cfg<0, 4, 64, 64>(h, s);
+    else if (pl.bn == 48) launch_cfg<0, 4, 64, 48>(h, s);
+    else launch_cfg<0, 4, 64, 32>(h, s);
+  } else if (pl.tw == 32) {
+    if (pl.bn == 64) launch_cfg<0, 8, 32, 64>(h, s);
+    else if (pl.bn == 48) launch_cfg<0, 8, 32, 48>(h, s);
+    else launch_cfg<0, 8, 32, 32>(h, s);
+  } else {
+    launch_cfg<0, 8, 64, 32>(h, s);
   }
-  HC(0, 4, 64) HC(1, 8, 32)
-#undef HC
-  if (shape == 2) launch_cfg<8, 64, 32>(h, s);
   return cnnitmo_check_launch(what);
 }
 
 const char* halo_name(const FwdArgs& a) {
-  const int bn = halo_bn_for(a.N);
-  switch (halo_shape(bn) * 100 + bn) {
-    case 64: return "conv3x3_halo_kernel<4,64,64>";
-    case 48: return "conv3x3_halo_kernel<4,64,48>";
-    case 32: return "conv3x3_halo_kernel<4,64,32>";
-    case 164: return "conv3x3_halo_kernel<8,32,64>";
-    case 148: return "conv3x3_halo_kernel<8,32,48>";
-    case 132: return "conv3x3_halo_kernel<8,32,32>";
-    default: return "conv3x3_halo_kernel<8,64,32>";
-  }
+  HaloPlan pl;
+  if (!halo_plan(a, pl)) return "";
+  static thread_local char buf[64];
+  snprintf(buf, sizeof(buf), "halo_gemm_kernel<%d,%d,%d,%d>", pl.mode, pl.th, pl.tw, pl.bn);
+  return buf;
 }
 
-// BN partial-sum rows written by the halo kernel: one per 256 pixels of each
+// BN partial-sum rows written by the halo kernel: one per 256 GEMM rows of each
 // (possibly partial) tile.
 long halo_stat_rows(const FwdArgs& a) {
-  const int bn = halo_bn_for(a.N);
-  const int shape = halo_shape(bn);
-  const int th = shape == 0 ? 4 : 8, tw = shape == 1 ? 32 : 64;
-  const long tiles = (long)a.nimg * ((a.ho + th - 1) / th) * ((a.wo + tw - 1) / tw);
-  return tiles * (th * tw / 256);
+  HaloPlan pl;
+  if (!halo_plan(a, pl)) return 0;
+  const long tiles = (long)a.nimg * ((a.ho + pl.th - 1) / pl.th) * ((a.wo + pl.tw - 1) / pl.tw);
+  return tiles * (pl.th * pl.tw / 256);
 }

@@ -336,6 +336,15 @@ extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int ci
   return cnnitmo_fwd_stat_rows(dtype, a.M, cout);
 }
 
+extern "C" long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int cin, int cout) {
+  FwdArgs a = base_args();
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  a.cin = cin; a.N = 4 * cout; a.a_ld = cin; a.out_ld = cout; a.M = (long)n * h * w;
+  a.scatter = 1; a.cout = cout;
+  if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_stat_rows(a);
+  return cnnitmo_fwd_stat_rows(dtype, a.M, 4 * cout);
+}
+
 extern "C" int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols) {
   (void)dtype;
   if (!use_v1() && fwd2_handles(ncols)) return fwd2_stat_rows(m);
@@ -375,6 +384,29 @@ extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int 
   a.M = (long)n * h * w;
   static thread_local char buf[96];
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
+  const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
+  if (!use_v1() && fwd2_handles(a.N)) {
+    const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
+    snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,256x%d>", t, bn);
+  } else {
+    const Cfg c = pick_cfg(a.N);
+    snprintf(buf, sizeof(buf), "igemm_fwd_kernel<%s,%dx%d>", t, c.bm, c.bn);
+  }
+  return buf;
+}
+
+extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int w, int cin, int cout,
+                                                    int dgrad) {
+  FwdArgs a = base_args();
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  a.cin = dgrad ? cout : cin;
+  a.N = dgrad ? cin : 4 * cout;
+  a.a_ld = a.cin; a.out_ld = dgrad ? cin : cout; a.cout = cout;
+  a.scatter = dgrad ? 0 : 1;
+  if (dgrad) { a.ntaps = 4; a.scale = 2; a.hs = 2 * h; a.ws = 2 * w; }
+  a.M = (long)n * h * w;
+  if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
+  static thread_local char buf[96];
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
   if (!use_v1() && fwd2_handles(a.N)) {
     const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;

@@ -229,6 +229,8 @@ class BlockStage(Stage):
         m, ncols = self._gemm_rows(n)
         if self.kind == "c3":
             rows = ops.conv3x3_stat_rows(e.dt, n, self.vout.h, self.vout.w, self.cin, cout)
+        elif self.kind == "t2":
+            rows = ops.tconv_stat_rows(e.dt, n, self.vin.h, self.vin.w, self.cin, cout)
         else:
             rows = ops.fwd_stat_rows(e.dt, m, ncols)
         stats = torch.empty(rows * 2 * ncols, device=e.device, dtype=torch.float32)

@@ -80,6 +80,11 @@ def conv3x3_stat_rows(dt, n, h, w, cin, cout):
     return query("cnnitmo_conv3x3_stat_rows", dt, n, h, w, cin, cout)
 
 
+def tconv_stat_rows(dt, n, h, w, cin, cout):
+    """BN partial rows of tconv_fwd over an n x h x w input grid."""
+    return query("cnnitmo_tconv2x2_stat_rows", dt, n, h, w, cin, cout)
+
+
 def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx: View):
     call("cnnitmo_conv3x3_dgrad", dt, ptr(dz), n, h, w, cout, ptr(wflip), cin, dx.ptr, dx.ld, dx.off,
          stream_ptr())

@@ -79,12 +79,17 @@ int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off, int n, in
  * layer cin/cout) launches for these sizes (profiling labels; no GPU needed). */
 const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int w, int cin, int cout,
                                         int dgrad);
+/* Same for tconv2x2_fwd / _dgrad over an n x h x w input grid. */
+const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int w, int cin, int cout,
+                                         int dgrad);
 
 /* Rows of the BN partial-sum buffer written by a forward conv over m output
  * pixels with ncols GEMM columns (4*cout for tconv2x2; the 1-tap first layer).
  * conv3x3: use cnnitmo_conv3x3_stat_rows (the row count depends on the frame). */
 int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols);
 long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int cin, int cout);
+/* Same for cnnitmo_tconv2x2_fwd over an n x h x w input grid (columns 4*cout). */
+long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int cin, int cout);
 
 /* Input-gradient of conv3x3 (TF Conv2DBackpropInput).  dz: [n,h,w,cout]
  * contiguous; wt_flip: [cin][3][3][cout] = W[co][2-r][2-s][ci] (from

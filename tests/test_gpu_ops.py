@@ -150,7 +150,7 @@ def test_tconv(dt, cin, cout, H, W):
     # output into a concat slice: ld = cout + 64, off = 64
     ld = cout + 64
     ob = torch.zeros(N * 2 * H * 2 * W * ld, dtype=TDT[dt], device="cuda")
-    rows = ops.fwd_stat_rows(d, N * H * W, 4 * cout)
+    rows = ops.tconv_stat_rows(d, N, H, W, cin, cout)
     stats = torch.zeros(rows, 2, 4 * cout, device="cuda")
     xv = ops.View(dev(x, dt).reshape(-1), N, H, W, cin, cin)
     ops.tconv_fwd(d, xv, kf, torch.tensor(b).cuda(), ops.View(ob, N, 2 * H, 2 * W, cout, ld, 64),

@@ -37,9 +37,9 @@ def unmangle(n):
 
 def label(name):
     n = unmangle(name.replace(" ", ""))
-    m = re.search(r"conv3x3_halo_kernel<(\d+),(\d+),(\d+),\d+>", n)
+    m = re.search(r"halo_gemm_kernel<(\d+),(\d+),(\d+),(\d+),\d+>", n)
     if m:
-        return "conv3x3_halo_kernel<%s,%s,%s>" % m.groups()
+        return "halo_gemm_kernel<%s,%s,%s,%s>" % m.groups()
     m = re.search(r"wgrad_halo_kernel<(\d+),(\d+),(\d+),", n)
     if m:
         return "wgrad_halo_kernel<%s,%s,%s>" % m.groups()
