@@ -283,7 +283,8 @@ def main():
             cpu = {"error": repr(e)}
 
     if rank == 0:
-        metric = "1080p SDR->HDR frames/sec (fwd+bwd)" if args.mode == "train" else "1080p SDR->HDR frames/sec (fwd)"
+        res = "1080p" if (args.height, args.width) == (1080, 1920) else f"{args.width}x{args.height}"
+        metric = f"{res} SDR->HDR frames/sec (fwd+bwd)" if args.mode == "train" else f"{res} SDR->HDR frames/sec (fwd)"
         line = {"metric": metric, "value": round(fps, 3), "unit": "frames/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 2),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
