@@ -70,8 +70,9 @@ __device__ __forceinline__ int hswz(int row, int piece) {
 //           to output pixel (2y + tap/2, 2x + tap%2)
 template <int MODE, int TH, int TW, int BN, int ST>
 struct HaloCfg {
-  static constexpr int NWAVE = TH, NT = NWAVE * 64;
-  static constexpr int FM = TW / 16, FN = BN / 16;
+  static constexpr int NWAVE = TH <= 8 ? TH : 8, NT = NWAVE * 64;
+  static constexpr int RPW = TH / NWAVE;  // tile rows per wave
+  static constexpr int FMR = TW / 16, FM = RPW * FMR, FN = BN / 16;
   static constexpr int KT = MODE == 0 ? 9 : 1;  // taps
   static constexpr int PW = MODE == 0 ? TW + 2 : TW, PROWS = (MODE == 0 ? TH + 2 : TH) * PW;
   static constexpr int P_INSTR = ((PROWS + 15) / 16 + NWAVE - 1) / NWAVE * NWAVE;
@@ -81,7 +82,7 @@ struct HaloCfg {
   static constexpr int PATCH = P_INSTR * 1024;
   static constexpr int STAGE = PATCH + B_INSTR * 1024;
   static constexpr int CLD = BN + 8;  // C staging row (bf16), per wave TW rows
-  static constexpr int C_BYTES = NWAVE * TW * CLD * 2;
+  static constexpr int C_BYTES = NWAVE * RPW * TW * CLD * 2;
   // the epilogue stages C in the stage it just consumed when it fits, else in its own region
   static constexpr bool C_IN_STAGE = C_BYTES + NWAVE * BN * 8 <= STAGE;
   static constexpr int C_OFF = ST * STAGE;
@@ -99,11 +100,12 @@ struct HaloArgs {
 };
 
 template <int MODE, int TH, int TW, int BN, int ST>
-__global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
+__global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm_kernel(const HaloArgs h) {
   using C = HaloCfg<MODE, TH, TW, BN, ST>;
   constexpr int KT = C::KT;
   static_assert(C::SMEM <= 160 * 1024, "LDS");
   constexpr int NWAVE = C::NWAVE, FM = C::FM, FN = C::FN, STAGE = C::STAGE, PW = C::PW;
+  constexpr int RPW = C::RPW, FMR = C::FMR;
   constexpr int NPI = C::NPI, NBI = C::NBI;
   constexpr int CPR = BN / 8;  // 16-byte output pieces per pixel
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
   // compile-time; the swizzle bit of (rbase + c) depends only on (c & 7), so the
   // 8 residues are precomputed and c*64 becomes an immediate offset.
   const int frow = lane & 15, fpc = lane >> 4;
-  const int rbase = wave * PW + frow;
+  const int rbase = wave * RPW * PW + frow;
   int apre[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) apre[k] = rbase * 64 + ((fpc ^ ((((rbase + k) >> 2) & 1) << 1)) << 4);
@@ -225,9 +227,9 @@ __global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
       const int r = MODE == 0 ? tap / 3 : 0, s = MODE == 0 ? tap - 3 * (tap / 3) : 0;
       uint4 af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int c = r * PW + i * 16 + s;
-        af[i] = *reinterpret_cast<const uint4*>(Ps + apre[c & 7] + c * 64);
+      for (int f = 0; f < FM; ++f) {
+        const int c = (f / FMR + r) * PW + (f % FMR) * 16 + s;  // tile row f/FMR of this wave
+        af[f] = *reinterpret_cast<const uint4*>(Ps + apre[c & 7] + c * 64);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j)
@@ -244,10 +246,9 @@ __global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
   auto epilogue = [&](const Pos& e, int buf) {
     const int img = e.img, y0 = e.y0, x0 = e.x0;
     const int n0 = e.nb * BN;
-    const int oh = y0 + wave;
-    const bool rowok = oh < p.ho;
+    const int oh0 = y0 + wave * RPW;  // first tile row of this wave
     char* cbase = C::C_IN_STAGE ? smem + buf * STAGE : smem + C::C_OFF;
-    bf16* Cs = reinterpret_cast<bf16*>(cbase) + wave * TW * C::CLD;
+    bf16* Cs = reinterpret_cast<bf16*>(cbase) + wave * RPW * TW * C::CLD;
     float* red = reinterpret_cast<float*>(cbase + C::C_BYTES);  // [NWAVE][BN][2]
     // MODE 1: this column block is one tap of the tconv (BN divides cout)
     const int tap1 = MODE == 1 ? n0 / p.cout : 0, co0 = MODE == 1 ? n0 - tap1 * p.cout : n0;
@@ -261,18 +262,19 @@ __global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
       const float* U = p.border ? p.border + (size_t)n * 8 : nullptr;
       s1[j] = s2[j] = 0.f;
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+      for (int f = 0; f < FM; ++f)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int col = i * 16 + (lane >> 4) * 4 + r;  // pixel within the wave's row
-          float v = acc[i][j][r] + bj;
+          const int rr = f / FMR, col = (f % FMR) * 16 + (lane >> 4) * 4 + r;  // pixel (row rr, col) of the wave
+          const int oh = oh0 + rr;
+          float v = acc[f][j][r] + bj;
           if (U) v -= border_corr(U, oh, x0 + col, p.ho, p.wo);
           if (relu) v = fmaxf(v, 0.f);
           if (aff) v = v * sj + hj;
-          const float vs = (rowok && x0 + col < p.wo) ? v : 0.f;  // partial tiles: valid pixels only
+          const float vs = (oh < p.ho && x0 + col < p.wo) ? v : 0.f;  // partial tiles: valid pixels only
           s1[j] += vs;
           s2[j] += vs * vs;
-          Cs[col * C::CLD + j * 16 + (lane & 15)] = from_f32<bf16>(v);
+          Cs[(rr * TW + col) * C::CLD + j * 16 + (lane & 15)] = from_f32<bf16>(v);
         }
     }
     if (stats) {
@@ -310,14 +312,15 @@ __global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
     // each wave stores its TW pixels x BN channels as 16-byte row pieces
     bf16* __restrict__ O = (bf16*)p.out;
     // MODE 0: output pixel (oh, x0 + col); MODE 1: (2*oh + tap/2, 2*(x0 + col) + tap%2) of the 2x grid
-    const long mrow = MODE == 0 ? ((long)img * p.ho + oh) * p.wo + x0
-                                : ((long)img * 2 * p.ho + 2 * oh + (tap1 >> 1)) * 2 * p.wo + 2 * x0 + (tap1 & 1);
     constexpr int PSTEP = MODE == 0 ? 1 : 2;  // output pixels per GEMM row step
 #pragma unroll
-    for (int idx = lane; idx < TW * CPR; idx += 64) {
-      const int col = idx / CPR, cc = idx - col * CPR;
-      const uint4 v = *reinterpret_cast<const uint4*>(Cs + col * C::CLD + cc * 8);
-      uint4* dst = (rowok && x0 + col < p.wo)
+    for (int idx = lane; idx < RPW * TW * CPR; idx += 64) {
+      const int px = idx / CPR, cc = idx - px * CPR;
+      const int rr = px / TW, col = px - rr * TW, oh = oh0 + rr;
+      const long mrow = MODE == 0 ? ((long)img * p.ho + oh) * p.wo + x0
+                                  : ((long)img * 2 * p.ho + 2 * oh + (tap1 >> 1)) * 2 * p.wo + 2 * x0 + (tap1 & 1);
+      const uint4 v = *reinterpret_cast<const uint4*>(Cs + px * C::CLD + cc * 8);
+      uint4* dst = (oh < p.ho && x0 + col < p.wo)
                        ? reinterpret_cast<uint4*>(O + (size_t)(mrow + PSTEP * col) * p.out_ld + p.out_off + co0 + cc * 8)
                        : h_sink + lane;
       *dst = v;
@@ -332,7 +335,8 @@ __global__ __launch_bounds__(TH * 64) void halo_gemm_kernel(const HaloArgs h) {
   // count is a lower bound for waves whose stats stores were exec-masked off,
   // which only makes their wait stricter.
   constexpr int L = NPI + NBI;
-  constexpr int NST = (TW * CPR + 63) / 64;  // output store instructions per wave
+  constexpr int NST = (RPW * TW * CPR + 63) / 64;  // output store instructions per wave
+  static_assert(RPW * TW * CPR % 64 == 0, "every lane issues the same number of stores");
   // BN partial sums are stored by threads tid < SG*BN: waves 0 .. (SG*BN-1)/64
   const int S = NST + ((stats && wave * 64 < C::SG * BN) ? 2 : 0);
   Pos ep = ip;  // position of the item being computed
@@ -379,11 +383,11 @@ void launch_cfg(const HaloArgs& h, hipStream_t s) {
   // one workgroup per CU (LDS-limited); as many ring stages as fit in 160 KB
   const dim3 grid((unsigned)((h.npairs + h.per_block - 1) / h.per_block));
   if constexpr (HaloCfg<MODE, TH, TW, BN, 5>::SMEM <= 160 * 1024)
-    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 5>), grid, dim3(TH * 64), 0, s, h);
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 5>), grid, dim3((HaloCfg<MODE, TH, TW, BN, 2>::NT)), 0, s, h);
   else if constexpr (HaloCfg<MODE, TH, TW, BN, 3>::SMEM <= 160 * 1024)
-    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 3>), grid, dim3(TH * 64), 0, s, h);
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 3>), grid, dim3((HaloCfg<MODE, TH, TW, BN, 2>::NT)), 0, s, h);
   else
-    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 2>), grid, dim3(TH * 64), 0, s, h);
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 2>), grid, dim3((HaloCfg<MODE, TH, TW, BN, 2>::NT)), 0, s, h);
 }
 
 int halo_cfg_env() {
@@ -415,12 +419,13 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
     if (force == 32 && a.N % 32 == 0) pl.bn = 32;
     else pl.bn = a.N % 64 == 0 ? 64 : (a.N % 48 == 0 ? 48 : (a.N % 32 == 0 ? 32 : 0));
     if (!pl.bn) return false;
-    // tile: 0 = 4x64 (4 waves), 1 = 8x32 (8 waves), 2 = 8x64 (8 waves, BN = 32 only)
+    // tile: 0 = 4x64 (4 waves), 1 = 8x32 (8 waves), 2 = 8x64 (8 waves, BN = 32 only),
+    //       3 = 16x32 (8 waves x 2 rows: twice the pixels per weight-tile load)
     const int e = halo_cfg_env();
-    int shape = pl.bn == 32 ? 2 : 1;
-    if (e >= 1 && e <= 3 && (e != 3 || pl.bn == 32)) shape = e - 1;
-    pl.th = shape == 0 ? 4 : 8;
-    pl.tw = shape == 1 ? 32 : 64;
+    int shape = 3;  // measured fastest for every BN (tools/bench_layers.py)
+    if (e >= 1 && e <= 4 && (e != 3 || pl.bn == 32)) shape = e - 1;
+    pl.th = shape == 0 ? 4 : (shape == 3 ? 16 : 8);
+    pl.tw = (shape == 1 || shape == 3) ? 32 : 64;
     return true;
   }
   if (a.ntaps == 1 && a.scale == 1 && a.scatter && a.hs == a.ho && a.ws == a.wo && a.cout % 64 == 0 &&
@@ -470,6 +475,10 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
     if (pl.bn == 64) launch_cfg<0, 4, 64, 64>(h, s);
     else if (pl.bn == 48) launch_cfg<0, 4, 64, 48>(h, s);
     else launch_cfg<0, 4, 64, 32>(h, s);
+  } else if (pl.th == 16) {
+    if (pl.bn == 64) launch_cfg<0, 16, 32, 64>(h, s);
+    else if (pl.bn == 48) launch_cfg<0, 16, 32, 48>(h, s);
+    else launch_cfg<0, 16, 32, 32>(h, s);
   } else if (pl.tw == 32) {
     if (pl.bn == 64) launch_cfg<0, 8, 32, 64>(h, s);
     else if (pl.bn == 48) launch_cfg<0, 8, 32, 48>(h, s);
