@@ -250,13 +250,12 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm
     char* cbase = C::C_IN_STAGE ? smem + buf * STAGE : smem + C::C_OFF;
     bf16* Cs = reinterpret_cast<bf16*>(cbase) + wave * RPW * TW * C::CLD;
     float* red = reinterpret_cast<float*>(cbase + C::C_BYTES);  // [NWAVE][BN][2]
-    // MODE 1: this column block is one tap of the tconv (BN divides cout)
-    const int tap1 = MODE == 1 ? n0 / p.cout : 0, co0 = MODE == 1 ? n0 - tap1 * p.cout : n0;
+    // MODE 1: GEMM column n = tap*cout + co (a block may span several taps when BN > cout)
     float s1[FN], s2[FN];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + j * 16 + (lane & 15);
-      const int co = MODE == 1 ? co0 + j * 16 + (lane & 15) : n;
+      const int co = MODE == 1 ? n % p.cout : n;
       const float bj = p.bias ? p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : co] : 0.f;
       const float sj = aff ? p.aff_scale[co] : 1.f, hj = aff ? p.aff_shift[co] : 0.f;
       const float* U = p.border ? p.border + (size_t)n * 8 : nullptr;
@@ -317,11 +316,13 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm
     for (int idx = lane; idx < RPW * TW * CPR; idx += 64) {
       const int px = idx / CPR, cc = idx - px * CPR;
       const int rr = px / TW, col = px - rr * TW, oh = oh0 + rr;
+      const int n = n0 + cc * 8;  // first column of this 16-byte piece (8 | cout)
+      const int tp = MODE == 1 ? n / p.cout : 0, co = MODE == 1 ? n - tp * p.cout : n;
       const long mrow = MODE == 0 ? ((long)img * p.ho + oh) * p.wo + x0
-                                  : ((long)img * 2 * p.ho + 2 * oh + (tap1 >> 1)) * 2 * p.wo + 2 * x0 + (tap1 & 1);
+                                  : ((long)img * 2 * p.ho + 2 * oh + (tp >> 1)) * 2 * p.wo + 2 * x0 + (tp & 1);
       const uint4 v = *reinterpret_cast<const uint4*>(Cs + px * C::CLD + cc * 8);
       uint4* dst = (oh < p.ho && x0 + col < p.wo)
-                       ? reinterpret_cast<uint4*>(O + (size_t)(mrow + PSTEP * col) * p.out_ld + p.out_off + co0 + cc * 8)
+                       ? reinterpret_cast<uint4*>(O + (size_t)(mrow + PSTEP * col) * p.out_ld + p.out_off + co)
                        : h_sink + lane;
       *dst = v;
     }
@@ -428,10 +429,10 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
     pl.tw = (shape == 1 || shape == 3) ? 32 : 64;
     return true;
   }
-  if (a.ntaps == 1 && a.scale == 1 && a.scatter && a.hs == a.ho && a.ws == a.wo && a.cout % 64 == 0 &&
+  if (a.ntaps == 1 && a.scale == 1 && a.scatter && a.hs == a.ho && a.ws == a.wo && a.cout % 32 == 0 &&
       a.N == 4 * a.cout) {
     pl.mode = 1;
-    pl.bn = a.cout % 128 == 0 ? 128 : 64;  // a column block never straddles two taps
+    pl.bn = 128;  // a block may span taps: pieces are scattered one by one
     pl.th = 8;
     pl.tw = 32;
     return true;
