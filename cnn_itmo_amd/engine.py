@@ -281,29 +281,34 @@ class BlockStage(Stage):
                              self.drop_id, dz, part2)
         db = e.g(self.conv.name + "/bias")
         dw = e.g(self.conv.name + "/kernel")
+        psum = None
         if par:
             ops.colsum(part2, rows, 4 * cout, 4, db)
             psum = torch.empty(4 * cout, device=e.device, dtype=torch.float32)
             ops.colsum(part2, rows, 4 * cout, 1, psum)
         else:
             ops.colsum(part2, rows, cout, 1, db)
-        if self.kind == "c3in":
-            ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
-                           dw, dw_cols=27)
-        elif self.kind == "c3":
-            fold = None
-            if self.fold_active:
-                h, w = self.vout.h, self.vout.w
-                brows = ops.border_rows(n)
-                bpart = torch.empty(brows * 8 * cout, device=e.device, dtype=torch.float32)
-                ops.border_sums(e.dt, dz, n, h, w, cout, bpart)
-                bsum = torch.empty(8 * cout, device=e.device, dtype=torch.float32)
-                ops.colsum(bpart, brows, 8 * cout, 1, bsum)
-                fold = self.vin.coef() + (db, bsum)
-            ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold)
-        else:
-            fold = self.vin.coef() + (psum,) if par else None
-            ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold)
+        # The weight gradient is off the critical path (dz -> dgrad -> next BN backward):
+        # it runs on the engine's side stream, overlapping the HBM-bound BN passes and the
+        # dgrad on the compute stream.  Tensors it reads are recorded on that stream.
+        with e.side(dz, psum, getattr(self, "cols", None)):
+            if self.kind == "c3in":
+                ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
+                               dw, dw_cols=27)
+            elif self.kind == "c3":
+                fold = None
+                if self.fold_active:
+                    h, w = self.vout.h, self.vout.w
+                    brows = ops.border_rows(n)
+                    bpart = torch.empty(brows * 8 * cout, device=e.device, dtype=torch.float32)
+                    ops.border_sums(e.dt, dz, n, h, w, cout, bpart)
+                    bsum = torch.empty(8 * cout, device=e.device, dtype=torch.float32)
+                    ops.colsum(bpart, brows, 8 * cout, 1, bsum)
+                    fold = self.vin.coef() + (db, bsum)
+                ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold)
+            else:
+                fold = self.vin.coef() + (psum,) if par else None
+                ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold)
         if self.vin.needs_grad:
             if self.vin.ginit:
                 raise NotImplementedError(f"{self.name}: input gradient would need accumulation")
@@ -533,6 +538,9 @@ class Engine:
         self.weights_dirty = True
         self.step = 0
         self.grad_hook = None  # callable(lo, hi) after each stage's gradients are written
+        self._side = None  # side stream for weight gradients (CNNITMO_SIDE_STREAM=0: off)
+        self._side_on = os.environ.get("CNNITMO_SIDE_STREAM", "1") != "0"
+        self._side_keep = []
 
     # ---- parameter access ---------------------------------------------------
     def _slice(self, flat, table, key):
@@ -576,6 +584,28 @@ class Engine:
                 if isinstance(st, BlockStage):
                     st.prep()
             self.weights_dirty = False
+
+    # ---- streams -------------------------------------------------------------
+    def side(self, *tensors):
+        """Context running its work on the side stream after everything queued so far
+        on the compute stream; `tensors` (allocated on the compute stream) are kept
+        alive for it.  Without a side stream: a no-op context."""
+        import contextlib
+        if not self._side_on:
+            return contextlib.nullcontext()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        main = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(main)
+        # keep the inputs alive until join_side() instead of record_stream(): deferred
+        # frees of multi-GB blocks would defeat the caching allocator's reuse
+        self._side_keep.extend(t for t in tensors if t is not None)
+        return torch.cuda.stream(self._side)
+
+    def join_side(self):
+        if self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+        self._side_keep.clear()
 
     # ---- execution ----------------------------------------------------------
     def _input(self, x):
@@ -621,12 +651,15 @@ class Engine:
         head = self.stages[-1]
         head.loss_and_grad(n, target.contiguous().float(), loss_acc)
         if self.grad_hook:
-            self.grad_hook(*self.stage_goff[-1])
+            with self.side():  # hooks (DP all-reduce launches) follow both streams' writes
+                self.grad_hook(*self.stage_goff[-1])
         for i in range(len(self.stages) - 2, -1, -1):
             st = self.stages[i]
             st.backward(n)
             if self.grad_hook and st.params:
-                self.grad_hook(*self.stage_goff[i])
+                with self.side():
+                    self.grad_hook(*self.stage_goff[i])
+        self.join_side()
         self._release()
         if sync is not None:
             sync()
