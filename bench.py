@@ -123,15 +123,15 @@ class KernelTimer:
             k = ops.query("cnnitmo_wgrad_kernel_name", dt, ntaps, n, h, w, cin, cout).decode()
             return k + " + slab_reduce"
 
-        def conv_wgrad(dt, ntaps, x, dz, cout, dw, dw_cols=0, fold=None):
+        def conv_wgrad(dt, ntaps, x, dz, cout, dw, *a, **k):
             fl = 2.0 * x.p * cout * (27 if ntaps == 1 else 9 * x.c)
             return self._bracket(wname(dt, ntaps, x.n, x.h, x.w, x.c, cout), fl, o["conv_wgrad"],
-                                 dt, ntaps, x, dz, cout, dw, dw_cols, fold)
+                                 dt, ntaps, x, dz, cout, dw, *a, **k)
 
-        def tconv_wgrad(dt, x, dout, cout, dk, fold=None):
+        def tconv_wgrad(dt, x, dout, cout, dk, *a, **k):
             fl = 2.0 * x.p * 4 * cout * x.c
             return self._bracket(wname(dt, 4, x.n, x.h, x.w, x.c, cout), fl, o["tconv_wgrad"],
-                                 dt, x, dout, cout, dk, fold)
+                                 dt, x, dout, cout, dk, *a, **k)
 
         for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad), ("tconv_fwd", tconv_fwd),
                      ("tconv_dgrad", tconv_dgrad), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),

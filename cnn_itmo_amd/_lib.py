@@ -38,12 +38,12 @@ SIGNATURES = {
     "cnnitmo_fwd_stat_rows": (i32, [i32, i64, i32]),
     "cnnitmo_conv3x3_dgrad": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, vp]),
     "cnnitmo_wgrad_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32, i32]),
-    "cnnitmo_conv_wgrad": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
+    "cnnitmo_conv_wgrad": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, sz, vp]),
     "cnnitmo_im2col_c3": (i32, [i32, vp, i32, i32, i32, i32, vp, vp]),
     "cnnitmo_conv1tap_fwd": (i32, [i32, vp, i32, i64, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_tconv2x2_fwd": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_tconv2x2_dgrad": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, vp]),
-    "cnnitmo_tconv2x2_wgrad": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, sz, vp]),
+    "cnnitmo_tconv2x2_wgrad": (i32, [i32, vp, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, sz, vp]),
     "cnnitmo_tconv2x2_wgrad_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32]),
     "cnnitmo_prep_conv3x3_weights": (i32, [i32, vp, i32, i32, vp, vp, vp]),
     "cnnitmo_prep_tconv2x2_weights": (i32, [i32, vp, i32, i32, vp, vp, vp]),
@@ -62,7 +62,9 @@ SIGNATURES = {
     "cnnitmo_head_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_head_rows": (i32, [i64]),
     "cnnitmo_head_fwd_bwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
-    "cnnitmo_head_finalize": (i32, [vp, i64, i32, f64, vp, vp, vp, vp, vp, vp, vp]),
+    "cnnitmo_head_finalize": (i32, [vp, i64, i32, f64, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "cnnitmo_bn_consumer_sums": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    "cnnitmo_pool_bnsums": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_fold_conv3x3": (i32, [i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_fold_tconv2x2": (i32, [i32, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
     "cnnitmo_border_rows": (i32, [i32]),

@@ -1,3 +1,4 @@
+#include <cstdlib>
 // HBM-bound kernels of the U-Net step: BatchNormalization (train/infer, fwd/bwd),
 // ReLU gradient, Dropout, MaxPooling2D fwd/bwd, the sigmoid head with MSE loss
 // and 'accuracy', RMSprop, weight preparation, first-layer packing and the
@@ -218,9 +219,18 @@ extern "C" int cnnitmo_bn_apply(int dtype, const void* r, long p, int c, const f
 // ----------------------------------------------------------------------------
 static constexpr int BWD_BLOCKS = 1024;
 
+static int bwd_blocks() {
+  static const int v = [] {
+    const char* e = getenv("CNNITMO_BWD_BLOCKS");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 ? x : BWD_BLOCKS;
+  }();
+  return v;
+}
+
 extern "C" int cnnitmo_bn_bwd_rows(long p, int c) {
   (void)c;
-  return (int)std::max<long>(1, std::min<long>(BWD_BLOCKS, (p + 7) / 8));
+  return (int)std::max<long>(1, std::min<long>(bwd_blocks(), (p + 7) / 8));
 }
 
 template <typename T>
@@ -706,7 +716,7 @@ extern "C" int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int 
 // Folded input BN (x = r, y = r*s + h): dW[o][c] = s[c]*sum(dz*r) + h[c]*db[o].
 __global__ void head_final_kernel(const double* __restrict__ ws, int G, int cin, double numel,
                                   float* loss_acc, float* dw, float* db, const float* fs,
-                                  const float* fh) {
+                                  const float* fh, float* raw) {
   const int ncol = 5 + 3 * cin;
   const int k = wave_col();
   if (k < ncol) {
@@ -720,17 +730,19 @@ __global__ void head_final_kernel(const double* __restrict__ ws, int G, int cin,
     else {
       const int c = (k - 5) % cin;
       dw[k - 5] = (float)((fs ? s * fs[c] : s) + (fh ? dbo * fh[c] : 0.0));
+      if (raw) raw[k - 5] = (float)s;
     }
   }
 }
 
 extern "C" int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
                                      const float* scale, const float* shift, float* loss_acc,
-                                     float* dw, float* db, void* workspace, void* stream) {
+                                     float* dw, float* db, float* raw_out, void* workspace,
+                                     void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int G = colsum_stage1_launch(part, rows, 5 + 3 * cin, workspace, s);
   hipLaunchKernelGGL(head_final_kernel, dim3(wave_grid(5 + 3 * cin)), dim3(256), 0, s, (const double*)workspace, G, cin,
-                     numel, loss_acc, dw, db, scale, shift);
+                     numel, loss_acc, dw, db, scale, shift, raw_out);
   return cnnitmo_check_launch("head_finalize");
 }
 
@@ -1053,4 +1065,136 @@ extern "C" int cnnitmo_border_sums(int dtype, const void* dz, int n, int h, int 
   else
     hipLaunchKernelGGL(border_sums_kernel<float>, dim3(n * BS_SEG), dim3(256), 0, s, (const float*)dz, h, w, c, part);
   return cnnitmo_check_launch("border_sums");
+}
+
+// ----------------------------------------------------------------------------
+// BN-backward sums without a pass over the activations.  For a BN output v whose
+// gradient is the input-gradient of a linear consumer (conv3x3 'same', tconv2x2,
+// the 1x1 head), both sums the BN backward needs follow from quantities the
+// consumer's weight gradient already produced:
+//   sum_q dy[q][ci]             = sum_{co,t} W[co][t][ci] * V[co][t]
+//   sum_q dy[q][ci] * rhat[q][ci] = inv[ci] * sum_{co,t} W[co][t][ci] * (raw[co][t][ci] - mean[ci] * V[co][t])
+// raw = sum_p dz[p][co] * r[p + off_t][ci] (zero padded) and V[co][t] = the sum of dz
+// over the pixels whose tap t lands inside the image (conv: db - border sums;
+// tconv: the per-tap parity sums; head: db).  Exact in real arithmetic (the
+// dgrad is the transpose of the same linear map), O(weights) work.
+// part[0][c] = sum dy, part[1][c] = sum dy * rhat (one row for cnnitmo_bn_bwd_finalize).
+// mode 1: conv3x3, w/raw [cout][9][cin_tot], V from db[cout] and border sums bs[8][cout]
+// mode 2: tconv2x2, w/raw [4][cout][cin_tot], V = par[4*cout]
+// mode 3: head 1x1, w/raw [3][cin_tot], V = db[3]
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ double conv_v(const float* db, const float* bs, int C, int co, int t) {
+  const int r = t / 3, q = t - 3 * r;
+  double o = 0.0;
+  if (r == 0) o += bs[0 * C + co];
+  if (r == 2) o += bs[1 * C + co];
+  if (q == 0) o += bs[2 * C + co];
+  if (q == 2) o += bs[3 * C + co];
+  if (r == 0 && q == 0) o -= bs[4 * C + co];
+  if (r == 0 && q == 2) o -= bs[5 * C + co];
+  if (r == 2 && q == 0) o -= bs[6 * C + co];
+  if (r == 2 && q == 2) o -= bs[7 * C + co];
+  return (double)db[co] - o;
+}
+
+__global__ void bn_consumer_sums_kernel(int mode, const float* __restrict__ w, const float* __restrict__ raw,
+                                        int cout, int cin_tot, int ci0, int c, const float* __restrict__ db,
+                                        const float* __restrict__ vt, const float* __restrict__ mean,
+                                        const float* __restrict__ inv, float* __restrict__ part) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= c) return;
+  const int ci = ci0 + j;
+  const int ntap = mode == 1 ? 9 : (mode == 2 ? 4 : 1);
+  double swv = 0.0, swr = 0.0;
+  for (int co = 0; co < cout; ++co)
+    for (int t = 0; t < ntap; ++t) {
+      size_t idx;
+      double v;
+      if (mode == 1) {
+        idx = ((size_t)co * 9 + t) * cin_tot + ci;
+        v = conv_v(db, vt, cout, co, t);
+      } else if (mode == 2) {
+        idx = ((size_t)t * cout + co) * cin_tot + ci;
+        v = vt[t * cout + co];
+      } else {
+        idx = (size_t)co * cin_tot + ci;
+        v = db[co];
+      }
+      const double wv = w[idx];
+      swv += wv * v;
+      swr += wv * raw[idx];
+    }
+  part[j] = (float)swv;
+  part[c + j] = (float)(inv[j] * (swr - (double)mean[j] * swv));
+}
+
+extern "C" int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* raw, int cout, int cin_tot,
+                                        int ci0, int c, const float* db, const float* vtab,
+                                        const float* mean, const float* invstd, float* part,
+                                        void* stream) {
+  CNN_REQUIRE(mode >= 1 && mode <= 3 && ci0 >= 0 && ci0 + c <= cin_tot && (mode == 2 || db),
+              "bn_consumer_sums: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_consumer_sums_kernel, dim3((c + 63) / 64), dim3(64), 0, s, mode, w, raw, cout,
+                     cin_tot, ci0, c, db, vtab, mean, invstd, part);
+  return cnnitmo_check_launch("bn_consumer_sums");
+}
+
+// The MaxPooling2D share of the same sums for a pooled BN output: the pool routes
+// dy_pool[p] to the argmax pixel of window p, so it adds sum_p dy_pool[p] and
+// sum_p dy_pool[p] * rhat[argmax(p)] (r read at the argmax only).
+// part rows: cnnitmo_bn_bwd_rows(p_pool, c).
+template <typename T>
+__global__ void pool_bnsums_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, int H, int W,
+                                   long Pp, int C, const T* __restrict__ r, long r_ld, int r_off,
+                                   const float* __restrict__ mean, const float* __restrict__ inv,
+                                   float* __restrict__ part) {
+  constexpr int VE = Vec16<T>::N;
+  const int tpp = C / VE, rows = 256 / tpp;
+  const int tid = threadIdx.x;
+  const int row = tid / tpp, cv = tid - row * tpp, c0 = cv * VE;
+  const int Ho = H / 2, Wo = W / 2;
+  float acc[2][VE];
+  float mu[VE], is[VE];
+#pragma unroll
+  for (int e = 0; e < VE; ++e) {
+    acc[0][e] = acc[1][e] = 0.f;
+    mu[e] = row < rows ? mean[c0 + e] : 0.f;
+    is[e] = row < rows ? inv[c0 + e] : 0.f;
+  }
+  if (row < rows) {
+    for (long po = (long)blockIdx.x * rows + row; po < Pp; po += (long)gridDim.x * rows) {
+      const int n = (int)(po / ((long)Ho * Wo));
+      const int rem = (int)(po - (long)n * Ho * Wo);
+      const int ho = rem / Wo, wo = rem - ho * Wo;
+      float g[VE];
+      Pack16<T>::load(dy + (size_t)po * C + c0, g);
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        const int k = idx[(size_t)po * C + c0 + e];
+        const long pin = ((long)n * H + 2 * ho + (k >> 1)) * W + 2 * wo + (k & 1);
+        const float rv = to_f32(r[(size_t)pin * r_ld + r_off + c0 + e]);
+        acc[0][e] += g[e];
+        acc[1][e] += g[e] * (rv - mu[e]) * is[e];
+      }
+    }
+  }
+  block_reduce_rows<VE, 2>(acc, C, part);
+}
+
+extern "C" int cnnitmo_pool_bnsums(int dtype, const void* dy, const uint8_t* idx, int n, int h, int w,
+                                   int c, const void* r, int r_ld, int r_off, const float* mean,
+                                   const float* invstd, float* part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long Pp = (long)n * (h / 2) * (w / 2);
+  const int G = cnnitmo_bn_bwd_rows(Pp, c);
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % VE == 0 && c / VE <= 256, "pool_bnsums: unsupported channel count %d", c);
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(pool_bnsums_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dy, idx, h, w, Pp, c,
+                       (const bf16*)r, (long)r_ld, r_off, mean, invstd, part);
+  else
+    hipLaunchKernelGGL(pool_bnsums_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dy, idx, h, w, Pp, c,
+                       (const float*)r, (long)r_ld, r_off, mean, invstd, part);
+  return cnnitmo_check_launch("pool_bnsums");
 }

@@ -280,6 +280,7 @@ struct WFold {
   const float* h;
   const float* db;  // mode 1: [cout]
   const float* v;   // mode 1: border sums [8][cout]; mode 2: parity sums [4*cout]
+  float* raw;       // optional: the uncorrected sum (gradient w.r.t. the folded weights' r-GEMM)
 };
 
 __device__ __forceinline__ float fold_v(const WFold& f, int row, int col) {
@@ -310,6 +311,7 @@ __global__ void slab_reduce_kernel(const float* __restrict__ ws, long slab, int 
     const long src = (long)row * cols_in + c;
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += ws[(size_t)k * slab + src];
+    if (f.raw) f.raw[i] = s;
     if (f.mode) {
       const int ci = c % f.cin;
       s = s * f.s[ci] + f.h[ci] * fold_v(f, row, c);
@@ -459,10 +461,10 @@ extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld,
                                   const void* dz, int n, int h, int w, int cin, int cout,
                                   float* dw, int dw_cols, const float* fold_scale,
                                   const float* fold_shift, const float* fold_db,
-                                  const float* fold_border, void* workspace, size_t ws_bytes,
-                                  void* stream) {
+                                  const float* fold_border, float* raw_out, void* workspace,
+                                  size_t ws_bytes, void* stream) {
   CNN_REQUIRE(ntaps == 9 || ntaps == 1, "conv_wgrad: ntaps must be 9 or 1");
-  WFold f{0, cin, cout, fold_scale, fold_shift, fold_db, fold_border};
+  WFold f{0, cin, cout, fold_scale, fold_shift, fold_db, fold_border, raw_out};
   if (fold_scale) {
     CNN_REQUIRE(ntaps == 9 && fold_shift && fold_db && fold_border && (dw_cols <= 0 || dw_cols == 9 * cin),
                 "conv_wgrad: folded BN needs ntaps 9, shift, db and border sums");
@@ -508,9 +510,9 @@ extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld,
 
 extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h,
                                       int w, int cin, int cout, float* dk, const float* fold_scale,
-                                      const float* fold_shift, const float* fold_par,
+                                      const float* fold_shift, const float* fold_par, float* raw_out,
                                       void* workspace, size_t ws_bytes, void* stream) {
-  WFold f{0, cin, cout, fold_scale, fold_shift, nullptr, fold_par};
+  WFold f{0, cin, cout, fold_scale, fold_shift, nullptr, fold_par, raw_out};
   if (fold_scale) {
     CNN_REQUIRE(fold_shift && fold_par, "tconv2x2_wgrad: folded BN needs shift and parity sums");
     f.mode = 2;

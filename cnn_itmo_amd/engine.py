@@ -57,6 +57,9 @@ class Value:
         self.ginit = False
         self.needs_grad = True
         self.folded = False  # holds r; the true value is r*cs + ch (per channel)
+        self.producer = None  # BlockStage writing this value
+        self.sum_consumers = 0  # >0: BN-backward sums come from this many consumers (no reduce pass)
+        self.bn_contrib = []  # per-step partial-sum tensors [rows][2][c] from the consumers
         self.cs = None  # coefficient buffers of the owner (persist across steps)
         self.ch = None
 
@@ -201,6 +204,17 @@ class BlockStage(Stage):
             return n * self.vin.h * self.vin.w, 4 * self.cout
         return n * self.vout.h * self.vout.w, self.cout
 
+    def _sum_targets(self):
+        """(value, channel offset) of this stage's inputs whose BN-backward sums it supplies."""
+        if self.kind == "c3in":
+            return []
+        members = self.vin.members if self.vin.members else [self.vin]
+        out = []
+        for m in members:
+            if m.sum_consumers:
+                out.append((m, m.place[1] if m.place else 0))
+        return out
+
     def forward(self, n, training):
         e = self.eng
         cout = self.cout
@@ -269,11 +283,20 @@ class BlockStage(Stage):
         flags = (L.DROPOUT if self.drop is not None else 0) | (L.PARITY if par else 0)
         if self.bn is not None:
             bn = self.bn
-            part = torch.empty(rows * 2 * cout, device=e.device, dtype=torch.float32)
-            ops.bn_bwd_reduce(e.dt, dy, self.r, cout, self.smean, self.sinv, flags, e.drop_seed,
-                              self.drop_id, part)
+            v = self.vout
+            if v.sum_consumers and len(v.bn_contrib) == v.sum_consumers:
+                # sums from the consumers' weight gradients (cnnitmo_bn_consumer_sums): no pass over dy
+                e.join_side(keep=True)
+                part = torch.cat(v.bn_contrib)
+                prow = part.numel() // (2 * cout)
+            else:
+                part = torch.empty(rows * 2 * cout, device=e.device, dtype=torch.float32)
+                ops.bn_bwd_reduce(e.dt, dy, self.r, cout, self.smean, self.sinv, flags, e.drop_seed,
+                                  self.drop_id, part)
+                prow = rows
+            v.bn_contrib = []
             coef = torch.empty(3 * cout, device=e.device, dtype=torch.float32)
-            ops.bn_bwd_finalize(part, rows, cout, P, e.p(bn.name + "/gamma"), self.smean, self.sinv,
+            ops.bn_bwd_finalize(part, prow, cout, P, e.p(bn.name + "/gamma"), self.smean, self.sinv,
                                 e.g(bn.name + "/gamma"), e.g(bn.name + "/beta"), coef)
             ops.bn_bwd_apply(e.dt, dy, self.r, cout, coef, flags, e.drop_seed, self.drop_id, dz, part2)
         else:
@@ -291,7 +314,9 @@ class BlockStage(Stage):
         # The weight gradient is off the critical path (dz -> dgrad -> next BN backward):
         # it runs on the engine's side stream, overlapping the HBM-bound BN passes and the
         # dgrad on the compute stream.  Tensors it reads are recorded on that stream.
+        targets = self._sum_targets() if self.fold_active else []
         with e.side(dz, psum, getattr(self, "cols", None)):
+            raw = torch.empty_like(dw) if targets else None
             if self.kind == "c3in":
                 ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
                                dw, dw_cols=27)
@@ -305,10 +330,20 @@ class BlockStage(Stage):
                     bsum = torch.empty(8 * cout, device=e.device, dtype=torch.float32)
                     ops.colsum(bpart, brows, 8 * cout, 1, bsum)
                     fold = self.vin.coef() + (db, bsum)
-                ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold)
+                ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
+                for m, ci0 in targets:
+                    pm = torch.empty(2 * m.c, device=e.device, dtype=torch.float32)
+                    ops.bn_consumer_sums(1, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, db,
+                                         bsum, m.producer.smean, m.producer.sinv, pm)
+                    m.bn_contrib.append(pm)
             else:
                 fold = self.vin.coef() + (psum,) if par else None
-                ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold)
+                ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
+                for m, ci0 in targets:
+                    pm = torch.empty(2 * m.c, device=e.device, dtype=torch.float32)
+                    ops.bn_consumer_sums(2, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, None,
+                                         psum, m.producer.smean, m.producer.sinv, pm)
+                    m.bn_contrib.append(pm)
         if self.vin.needs_grad:
             if self.vin.ginit:
                 raise NotImplementedError(f"{self.name}: input gradient would need accumulation")
@@ -349,6 +384,13 @@ class PoolStage(Stage):
             if self.vin.place:
                 raise NotImplementedError("pool gradient into an uninitialised concat slice")
             self.vin.ensure_grad(n, e.tdtype, e.device, zero=True)
+        v = self.vin
+        if v.sum_consumers:  # this pool's share of the BN-backward sums of its input
+            pp = n * (v.h // 2) * (v.w // 2)
+            rows = ops.bn_bwd_rows(pp, v.c)
+            pm = torch.empty(rows * 2 * v.c, device=e.device, dtype=torch.float32)
+            ops.pool_bnsums(e.dt, self.vout.gbuf, self.idx, v.view(n), v.producer.smean, v.producer.sinv, pm)
+            v.bn_contrib.append(pm)
         ops.maxpool_bwd(e.dt, self.vout.gbuf, self.idx, self.vin.gview(n))
         self.idx = None
 
@@ -384,8 +426,16 @@ class HeadStage(Stage):
         aff = self.vin.coef() if e.training and self.vin.folded else None
         ops.head_fwd_bwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
                          e.p(self.name + "/bias"), target, dx.buf, part, aff)
+        v = self.vin
+        raw = torch.empty(3 * self.cin, device=e.device, dtype=torch.float32) \
+            if e.training and v.sum_consumers and v.folded else None
         ops.head_finalize(part, rows, self.cin, n * e.h_valid * self.vin.w * 3, loss_acc,
-                          e.g(self.name + "/kernel"), e.g(self.name + "/bias"), aff)
+                          e.g(self.name + "/kernel"), e.g(self.name + "/bias"), aff, raw=raw)
+        if raw is not None:
+            pm = torch.empty(2 * v.c, device=e.device, dtype=torch.float32)
+            ops.bn_consumer_sums(3, e.p(self.name + "/kernel"), raw, 3, self.cin, 0, v.c, e.g(self.name + "/bias"),
+                                 None, v.producer.smean, v.producer.sinv, pm)
+            v.bn_contrib.append(pm)
         self.vin.mark_grad()
 
 
@@ -464,6 +514,7 @@ def compile_graph(model, fold=True):
             vout.folded = fold and bn is not None and drop is None
             values[id(t)] = vout
             st = BlockStage(kind, l, relu, bn, drop, drop_id, values[id(x)], vout)
+            vout.producer = st
             stages.append(st)
         elif isinstance(l, MaxPooling2D):
             vout = Value(l.name, l.output.shape)
@@ -488,7 +539,34 @@ def compile_graph(model, fold=True):
             raise NotImplementedError(f"{l.name} ({type(l).__name__}) outside a fusable pattern")
     if not stages or not isinstance(stages[-1], HeadStage):
         raise NotImplementedError("the model must end in Conv2D(3, 1, activation='sigmoid')")
+    _plan_bn_sums(stages)
     return stages
+
+
+def _plan_bn_sums(stages):
+    """Mark the folded BN outputs whose backward sums (sum dy, sum dy*rhat) can be
+    assembled from their consumers instead of a pass over dy: every consumer must be a
+    conv3x3 / tconv / head (cnnitmo_bn_consumer_sums) or a MaxPooling2D
+    (cnnitmo_pool_bnsums).  Dropout outputs are materialised, hence never folded."""
+    readers = {}
+    for st in stages:
+        srcs = []
+        if isinstance(st, (BlockStage, PoolStage, HeadStage)):
+            srcs = [st.vin]
+        for v in srcs:
+            for m in (v.members if v.members else [v]):
+                readers.setdefault(id(m), []).append(st)
+    for st in stages:
+        if not isinstance(st, BlockStage) or st.bn is None or st.drop is not None:
+            continue
+        v = st.vout
+        if not v.folded:
+            continue
+        rs = readers.get(id(v), [])
+        ok = bool(rs) and all(
+            (isinstance(r, BlockStage) and r.kind in ("c3", "t2")) or isinstance(r, (PoolStage, HeadStage))
+            for r in rs)
+        v.sum_consumers = len(rs) if ok else 0
 
 
 def layout_params(stages):
@@ -602,10 +680,11 @@ class Engine:
         self._side_keep.extend(t for t in tensors if t is not None)
         return torch.cuda.stream(self._side)
 
-    def join_side(self):
+    def join_side(self, keep=False):
         if self._side is not None:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
-        self._side_keep.clear()
+        if not keep:
+            self._side_keep.clear()
 
     # ---- execution ----------------------------------------------------------
     def _input(self, x):

@@ -90,13 +90,14 @@ def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx: View):
          stream_ptr())
 
 
-def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0, fold=None):
-    """fold = (scale, shift, db, border_sums) for a folded input BN, else None."""
+def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0, fold=None, raw=None):
+    """fold = (scale, shift, db, border_sums) for a folded input BN, else None;
+    raw (optional, dw-shaped fp32): the uncorrected dz (x) r sum."""
     nbytes = query("cnnitmo_wgrad_workspace_bytes", dt, x.n, x.h, x.w, x.c, cout, ntaps)
     ws = workspace(nbytes, dz.device)
     fs, fh, fdb, fb = fold if fold is not None else (None,) * 4
     call("cnnitmo_conv_wgrad", dt, ntaps, x.ptr, x.ld, x.off, ptr(dz), x.n, x.h, x.w, x.c, cout,
-         ptr(dw), dw_cols, ptr(fs), ptr(fh), ptr(fdb), ptr(fb), ws.data_ptr(), ws.numel(),
+         ptr(dw), dw_cols, ptr(fs), ptr(fh), ptr(fdb), ptr(fb), ptr(raw), ws.data_ptr(), ws.numel(),
          stream_ptr())
 
 
@@ -115,14 +116,14 @@ def tconv_dgrad(dt, dout, n, h, w, cout, kT, cin, dx):
     call("cnnitmo_tconv2x2_dgrad", dt, ptr(dout), n, h, w, cout, ptr(kT), cin, ptr(dx), stream_ptr())
 
 
-def tconv_wgrad(dt, x: View, dout, cout, dk, fold=None):
+def tconv_wgrad(dt, x: View, dout, cout, dk, fold=None, raw=None):
     """fold = (scale, shift, parity_sums[4*cout]) for a folded input BN, else None."""
     assert x.ld == x.c and x.off == 0
     nbytes = query("cnnitmo_tconv2x2_wgrad_workspace_bytes", dt, x.n, x.h, x.w, x.c, cout)
     ws = workspace(nbytes, dout.device)
     fs, fh, fp = fold if fold is not None else (None,) * 3
     call("cnnitmo_tconv2x2_wgrad", dt, x.ptr, ptr(dout), x.n, x.h, x.w, x.c, cout, ptr(dk),
-         ptr(fs), ptr(fh), ptr(fp), ws.data_ptr(), ws.numel(), stream_ptr())
+         ptr(fs), ptr(fh), ptr(fp), ptr(raw), ws.data_ptr(), ws.numel(), stream_ptr())
 
 
 def prep_conv3x3(dt, w32, cout, cin, wf, wflip):
@@ -242,11 +243,24 @@ def head_rows(p):
     return query("cnnitmo_head_rows", p)
 
 
-def head_finalize(part, rows, cin, numel, loss_acc, dw, db, aff=None):
+def head_finalize(part, rows, cin, numel, loss_acc, dw, db, aff=None, raw=None):
     sc, sh = aff if aff is not None else (None, None)
     ws = reduce_ws(rows, 5 + 3 * cin, part.device)
     call("cnnitmo_head_finalize", ptr(part), rows, cin, float(numel), ptr(sc), ptr(sh),
-         ptr(loss_acc), ptr(dw), ptr(db), ws.data_ptr(), stream_ptr())
+         ptr(loss_acc), ptr(dw), ptr(db), ptr(raw), ws.data_ptr(), stream_ptr())
+
+
+def bn_consumer_sums(mode, w, raw, cout, cin_tot, ci0, c, db, vtab, mean, inv, part):
+    """part[2][c] = (sum dy, sum dy*rhat) of a BN output from its consumer's weight
+    gradient (mode 1 conv3x3, 2 tconv, 3 head); see cnn_itmo.h."""
+    call("cnnitmo_bn_consumer_sums", mode, ptr(w), ptr(raw), cout, cin_tot, ci0, c, ptr(db), ptr(vtab),
+         ptr(mean), ptr(inv), ptr(part), stream_ptr())
+
+
+def pool_bnsums(dt, dy, idx, vin: View, mean, inv, part):
+    """The MaxPooling2D share of those sums (rows = bn_bwd_rows(pooled pixels, c))."""
+    call("cnnitmo_pool_bnsums", dt, ptr(dy), ptr(idx), vin.n, vin.h, vin.w, vin.c, vin.ptr, vin.ld, vin.off,
+         ptr(mean), ptr(inv), ptr(part), stream_ptr())
 
 
 def rmsprop(p, g, a, lr, rho, eps, grad_scale=1.0):

@@ -109,13 +109,14 @@ const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, int h, int w,
 int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
                        const void* dz, int n, int h, int w, int cin, int cout, float* dw,
                        int dw_cols, const float* fold_scale, const float* fold_shift,
-                       const float* fold_db, const float* fold_border, void* workspace,
-                       size_t ws_bytes, void* stream);
+                       const float* fold_db, const float* fold_border, float* raw_out,
+                       void* workspace, size_t ws_bytes, void* stream);
 /* Folded input BN (x holds r, the conv's input is y = r*s + h, see
  * cnnitmo_fold_conv3x3): pass fold_scale = s, fold_shift = h [cin], fold_db = the
  * bias gradient [cout] and fold_border = the reduced border sums [8][cout] of dz
  * (cnnitmo_border_sums + cnnitmo_colsum); dw is then the exact gradient w.r.t. W.
- * All four NULL: plain weight gradient. */
+ * All four NULL: plain weight gradient.  raw_out (nullable, same layout as dw):
+ * the uncorrected sum dz (x) r, input of cnnitmo_bn_consumer_sums. */
 
 /* First layer (Cin=3): pack x [n,h_valid,w,3] fp32 into [n,h,w,32] dtype
  * columns k=(r*3+s)*3+c (k<27, zero pad; rows >= h_valid are zero), so that
@@ -146,8 +147,8 @@ int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h, int w, int
 /* dk [2][2][cout][cin] fp32 (OVERWRITTEN) from x [n,h,w,cin], dout [n,2h,2w,cout]. */
 int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h, int w,
                            int cin, int cout, float* dk, const float* fold_scale,
-                           const float* fold_shift, const float* fold_par, void* workspace,
-                           size_t ws_bytes, void* stream);
+                           const float* fold_shift, const float* fold_par, float* raw_out,
+                           void* workspace, size_t ws_bytes, void* stream);
 /* fold_par: per-tap sums of dout [4][cout] (cnnitmo_bn_bwd_apply with
  * CNNITMO_PARITY, reduced by cnnitmo_colsum); NULL trio = plain gradient. */
 size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin, int cout);
@@ -238,6 +239,21 @@ int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off, const
                          void* stream);
 /* r view: (r_ld, r_off).  part columns: [c], or [4][c] by pixel parity with
  * CNNITMO_PARITY (h, w = the spatial size, needed only then). */
+/* BN-backward sums WITHOUT a pass over dy: for a BN output whose gradient is the
+ * input-gradient of a linear consumer (mode 1 conv3x3, 2 tconv2x2, 3 the 1x1
+ * head), part[2][c] = {sum dy, sum dy*rhat} over the consumer's input channels
+ * [ci0, ci0+c) from its weights w, its uncorrected weight-gradient raw (raw_out of
+ * the *_wgrad / head_finalize call) and V (mode 1: db[cout] + border sums
+ * vtab[8][cout]; mode 2: parity sums vtab[4*cout]; mode 3: db[3]).  Exact: the
+ * dgrad is the transpose of the same map.  Feed to cnnitmo_bn_bwd_finalize.
+ * cnnitmo_pool_bnsums adds a MaxPooling2D consumer's share (rows =
+ * cnnitmo_bn_bwd_rows(n*(h/2)*(w/2), c)); r is the pooled tensor's view. */
+int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* raw, int cout, int cin_tot, int ci0,
+                             int c, const float* db, const float* vtab, const float* mean,
+                             const float* invstd, float* part, void* stream);
+int cnnitmo_pool_bnsums(int dtype, const void* dy, const uint8_t* idx, int n, int h, int w, int c,
+                        const void* r, int r_ld, int r_off, const float* mean, const float* invstd,
+                        float* part, void* stream);
 /* Column sums of partial rows -> out[groups-folded c] (fp32, written). */
 int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* out,
                    void* workspace, void* stream);
@@ -259,7 +275,7 @@ int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, in
                          void* stream);
 int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
                           const float* scale, const float* shift, float* loss_acc, float* dw,
-                          float* db, void* workspace, void* stream);
+                          float* db, float* raw_out, void* workspace, void* stream);
 /* scale/shift (nullable, [cin]): x holds r and the head's input is r*scale +
  * shift (folded BN); dx is then d/dy and dw the gradient w.r.t. the raw W. */
 
