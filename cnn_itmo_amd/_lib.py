@@ -21,6 +21,7 @@ DROPOUT = 1
 NO_BN = 2
 PARITY = 4
 BIAS_PER_COL = 8
+CONSUMER_ROWS = 16
 
 vp = C.c_void_p
 i32 = C.c_int
@@ -65,6 +66,8 @@ SIGNATURES = {
     "cnnitmo_head_finalize": (i32, [vp, i64, i32, f64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_bn_consumer_sums": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_pool_bnsums": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
+    "cnnitmo_bn_bwd_apply_pooled": (i32, [i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
+                                          vp, vp]),
     "cnnitmo_fold_conv3x3": (i32, [i32, vp, vp, vp, vp, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_fold_tconv2x2": (i32, [i32, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
     "cnnitmo_border_rows": (i32, [i32]),

@@ -352,12 +352,13 @@ extern "C" int cnnitmo_bn_bwd_finalize(const float* part, long rows, int c, doub
 // NP = 1: partial sums of dz per channel (bias gradient); NP = 4: split by the
 // pixel's (h&1, w&1) parity, i.e. per Conv2DTranspose tap of the producer
 // (needed by the folded-BN wgrad correction of the tconv; db = their sum).
-template <typename T, int NP>
+template <typename T, int NP, bool ROUTE>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, long dy_ld, int dy_off,
                                     const T* __restrict__ r, long r_ld, int r_off, long P, int C,
                                     const float* __restrict__ coef, int nobn, int drop,
                                     uint64_t dbase, T* __restrict__ dz, float* __restrict__ part,
-                                    int H, int W) {
+                                    int H, int W, const T* __restrict__ dyp,
+                                    const uint8_t* __restrict__ pidx) {
   constexpr int VE = Vec16<T>::N;
   const int tpp = C / VE, rows = 256 / tpp;
   const int tid = threadIdx.x;
@@ -378,6 +379,28 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, long dy_ld, int dy
       float g[VE], rv[VE];
       load_dy<T>(dy, dy_ld, dy_off, p, C, c0, drop, dbase, g);
       Pack16<T>::load(r + (size_t)p * r_ld + r_off + c0, rv);
+      if constexpr (ROUTE) {  // + the MaxPooling2D gradient routed to this pixel
+        const long hw = (long)H * W;
+        const int n = (int)(p / hw), rem = (int)(p - n * hw);
+        const int hh = rem / W, ww = rem - hh * W, Ho = H / 2, Wo = W / 2;
+        if ((hh >> 1) < Ho && (ww >> 1) < Wo) {
+          const long po = ((long)n * Ho + (hh >> 1)) * Wo + (ww >> 1);
+          const int k = ((hh & 1) << 1) | (ww & 1);
+          float gp[VE];
+          Pack16<T>::load(dyp + (size_t)po * C + c0, gp);
+          const uint8_t* ip = pidx + (size_t)po * C + c0;
+          uint8_t arg[VE];
+          if constexpr (VE == 8) {
+            const uint2 a2 = *(const uint2*)ip;
+            __builtin_memcpy(arg, &a2, 8);
+          } else {
+            const uint32_t a1 = *(const uint32_t*)ip;
+            __builtin_memcpy(arg, &a1, 4);
+          }
+#pragma unroll
+          for (int e = 0; e < VE; ++e) g[e] += arg[e] == k ? gp[e] : 0.f;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < VE; ++e) {
         const float d = rv[e] > 0.f ? (ca[e] * g[e] - cb[e] * rv[e] + ce[e]) : 0.f;
@@ -418,9 +441,9 @@ extern "C" int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy
   const bool par = flags & CNNITMO_PARITY;
   CNN_REQUIRE(!par || (h > 0 && w > 0), "bn_bwd_apply: PARITY needs h, w");
 #define BNA(T, NP)                                                                                \
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, NP>), dim3(G), dim3(256), 0, s, (const T*)dy,        \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, NP, false>), dim3(G), dim3(256), 0, s, (const T*)dy, \
                      (long)dy_ld, dy_off, (const T*)r, (long)r_ld, r_off, p, c, coef, nobn, drop, \
-                     base, (T*)dz, part, h, w)
+                     base, (T*)dz, part, h, w, nullptr, nullptr)
   if (dtype == CNNITMO_BF16) {
     if (par) BNA(bf16, 4); else BNA(bf16, 1);
   } else {
@@ -428,6 +451,27 @@ extern "C" int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy
   }
 #undef BNA
   return cnnitmo_check_launch("bn_bwd_apply");
+}
+
+extern "C" int cnnitmo_bn_bwd_apply_pooled(int dtype, const void* dy, int dy_ld, int dy_off, const void* r,
+                                           int r_ld, int r_off, int n, int h, int w, int c,
+                                           const float* coef, const void* dy_pool, const uint8_t* idx,
+                                           void* dz, float* part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const long p = (long)n * h * w;
+  const int G = cnnitmo_bn_bwd_rows(p, c);
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % 8 == 0 && c / VE <= 256 && dy_ld % 8 == 0 && dy_off % 8 == 0 && r_ld % 8 == 0 &&
+              r_off % 8 == 0 && coef && dy_pool && idx, "bn_bwd_apply_pooled: unsupported arguments (c=%d)", c);
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, 1, true>), dim3(G), dim3(256), 0, s, (const bf16*)dy,
+                       (long)dy_ld, dy_off, (const bf16*)r, (long)r_ld, r_off, p, c, coef, 0, 0, (uint64_t)0,
+                       (bf16*)dz, part, h, w, (const bf16*)dy_pool, idx);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, 1, true>), dim3(G), dim3(256), 0, s, (const float*)dy,
+                       (long)dy_ld, dy_off, (const float*)r, (long)r_ld, r_off, p, c, coef, 0, 0, (uint64_t)0,
+                       (float*)dz, part, h, w, (const float*)dy_pool, idx);
+  return cnnitmo_check_launch("bn_bwd_apply_pooled");
 }
 
 // ----------------------------------------------------------------------------
@@ -480,16 +524,16 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, long x_ld, int x_off
   }
 }
 
+// Rows of pooled pixels per 256-thread block: tpp = C/VE threads per pixel.
 template <typename T>
-__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, int N,
-                                   int H, int W, int C, T* __restrict__ dx, long dx_ld, int dx_off) {
+__global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, int H, int W,
+                                   long Pp, int C, T* __restrict__ dx, long dx_ld, int dx_off) {
   constexpr int VE = Vec16<T>::N;
-  const int Ho = H / 2, Wo = W / 2, cv = C / VE;
-  const long total = (long)N * Ho * Wo * cv;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const long po = i / cv;
-    const int c0 = (int)(i - po * cv) * VE;
+  const int tpp = C / VE, rows = 256 / tpp;
+  const int row = threadIdx.x / tpp, cv = threadIdx.x - row * tpp, c0 = cv * VE;
+  const int Ho = H / 2, Wo = W / 2;
+  if (row >= rows) return;
+  for (long po = (long)blockIdx.x * rows + row; po < Pp; po += (long)gridDim.x * rows) {
     const int n = (int)(po / ((long)Ho * Wo));
     const int rem = (int)(po - (long)n * Ho * Wo);
     const int ho = rem / Wo, wo = rem - ho * Wo;
@@ -516,6 +560,53 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
   }
 }
 
+// The MaxPooling2D share of the BN-backward sums of a folded pool input (see
+// cnnitmo_bn_consumer_sums): sum_p dyp[p] and sum_p dyp[p] * rhat[argmax(p)].
+// The 2x2 window of r is read whole (two coalesced pixel pairs) and the argmax
+// element selected per channel.
+template <typename T>
+__global__ void pool_bnsums_kernel(const T* __restrict__ dyp, const uint8_t* __restrict__ idx, int H, int W,
+                                   long Pp, int C, const T* __restrict__ r, long r_ld, int r_off,
+                                   const float* __restrict__ mean, const float* __restrict__ inv,
+                                   float* __restrict__ part) {
+  constexpr int VE = Vec16<T>::N;
+  const int tpp = C / VE, rows = 256 / tpp;
+  const int row = threadIdx.x / tpp, cv = threadIdx.x - row * tpp, c0 = cv * VE;
+  const int Ho = H / 2, Wo = W / 2;
+  float acc[2][VE], mu[VE], is[VE];
+#pragma unroll
+  for (int e = 0; e < VE; ++e) {
+    acc[0][e] = acc[1][e] = 0.f;
+    mu[e] = row < rows ? mean[c0 + e] : 0.f;
+    is[e] = row < rows ? inv[c0 + e] : 0.f;
+  }
+  if (row < rows) {
+    for (long po = (long)blockIdx.x * rows + row; po < Pp; po += (long)gridDim.x * rows) {
+      const int n = (int)(po / ((long)Ho * Wo));
+      const int rem = (int)(po - (long)n * Ho * Wo);
+      const int ho = rem / Wo, wo = rem - ho * Wo;
+      float g[VE], rw[4][VE];
+      Pack16<T>::load(dyp + (size_t)po * C + c0, g);
+      uint8_t arg[VE];
+#pragma unroll
+      for (int e = 0; e < VE; ++e) arg[e] = idx[(size_t)po * C + c0 + e];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const long pin = ((long)n * H + 2 * ho + (k >> 1)) * W + 2 * wo + (k & 1);
+        Pack16<T>::load(r + (size_t)pin * r_ld + r_off + c0, rw[k]);
+      }
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        const int k = arg[e];
+        const float rv = k == 0 ? rw[0][e] : (k == 1 ? rw[1][e] : (k == 2 ? rw[2][e] : rw[3][e]));
+        acc[0][e] += g[e];
+        acc[1][e] += g[e] * (rv - mu[e]) * is[e];
+      }
+    }
+  }
+  block_reduce_rows<VE, 2>(acc, C, part);
+}
+
 extern "C" int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h,
                                       int w, int c, void* y, uint8_t* idx, const float* scale,
                                       const float* shift, void* stream) {
@@ -531,18 +622,40 @@ extern "C" int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_
   return cnnitmo_check_launch("maxpool_fwd");
 }
 
-extern "C" int cnnitmo_maxpool2x2_bwd(int dtype, const void* dy, const uint8_t* idx, int n, int h,
-                                      int w, int c, void* dx, int dx_ld, int dx_off, void* stream) {
+extern "C" int cnnitmo_maxpool2x2_bwd(int dtype, const void* dy, const uint8_t* idx, int n, int h, int w,
+                                      int c, void* dx, int dx_ld, int dx_off, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  CNN_REQUIRE(c % 8 == 0 && dx_ld % 8 == 0 && dx_off % 8 == 0, "maxpool_bwd: channels must be multiples of 8");
-  const long work = (long)n * (h / 2) * (w / 2) * c;
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % 8 == 0 && dx_ld % 8 == 0 && dx_off % 8 == 0 && c / VE <= 256,
+              "maxpool_bwd: channels must be multiples of 8 (at most 1024/2048)");
+  const long Pp = (long)n * (h / 2) * (w / 2);
+  const int rows = 256 / (c / VE);
+  const int G = (int)std::max<long>(1, std::min<long>((Pp + rows - 1) / rows, 8192));
   if (dtype == CNNITMO_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(grid_for(work / 8)), dim3(256), 0, s,
-                       (const bf16*)dy, idx, n, h, w, c, (bf16*)dx, (long)dx_ld, dx_off);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dy, idx, h, w, Pp, c,
+                       (bf16*)dx, (long)dx_ld, dx_off);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(grid_for(work / 4)), dim3(256), 0, s,
-                       (const float*)dy, idx, n, h, w, c, (float*)dx, (long)dx_ld, dx_off);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dy, idx, h, w, Pp,
+                       c, (float*)dx, (long)dx_ld, dx_off);
   return cnnitmo_check_launch("maxpool_bwd");
+}
+
+extern "C" int cnnitmo_pool_bnsums(int dtype, const void* dyp, const uint8_t* idx, int n, int h, int w,
+                                   int c, const void* r, int r_ld, int r_off, const float* mean,
+                                   const float* invstd, float* part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % 8 == 0 && r_ld % 8 == 0 && r_off % 8 == 0 && c / VE <= 256,
+              "pool_bnsums: unsupported channel count %d", c);
+  const long Pp = (long)n * (h / 2) * (w / 2);
+  const int G = cnnitmo_bn_bwd_rows(Pp, c);
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL(pool_bnsums_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dyp, idx, h, w, Pp, c,
+                       (const bf16*)r, (long)r_ld, r_off, mean, invstd, part);
+  else
+    hipLaunchKernelGGL(pool_bnsums_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dyp, idx, h, w, Pp,
+                       c, (const float*)r, (long)r_ld, r_off, mean, invstd, part);
+  return cnnitmo_check_launch("pool_bnsums");
 }
 
 // ----------------------------------------------------------------------------
@@ -1097,35 +1210,40 @@ __device__ __forceinline__ double conv_v(const float* db, const float* bs, int C
   return (double)db[co] - o;
 }
 
+// Grid (c/64, CNNITMO_CONSUMER_ROWS); a block's 4 waves split its slice of the
+// K = cout*taps (co, tap) pairs (w/raw rows k*cin_tot, coalesced over ci) and
+// reduce in LDS; every grid row writes one partial row (linear in the slices).
 __global__ void bn_consumer_sums_kernel(int mode, const float* __restrict__ w, const float* __restrict__ raw,
                                         int cout, int cin_tot, int ci0, int c, const float* __restrict__ db,
                                         const float* __restrict__ vt, const float* __restrict__ mean,
                                         const float* __restrict__ inv, float* __restrict__ part) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= c) return;
-  const int ci = ci0 + j;
-  const int ntap = mode == 1 ? 9 : (mode == 2 ? 4 : 1);
+  const int cl = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
+  const int K = cout * (mode == 1 ? 9 : (mode == 2 ? 4 : 1));
+  const int slices = gridDim.y * 4, sl = blockIdx.y * 4 + sub;
+  const int k0 = (int)((long)K * sl / slices), k1 = (int)((long)K * (sl + 1) / slices);
   double swv = 0.0, swr = 0.0;
-  for (int co = 0; co < cout; ++co)
-    for (int t = 0; t < ntap; ++t) {
-      size_t idx;
-      double v;
-      if (mode == 1) {
-        idx = ((size_t)co * 9 + t) * cin_tot + ci;
-        v = conv_v(db, vt, cout, co, t);
-      } else if (mode == 2) {
-        idx = ((size_t)t * cout + co) * cin_tot + ci;
-        v = vt[t * cout + co];
-      } else {
-        idx = (size_t)co * cin_tot + ci;
-        v = db[co];
-      }
+  if (j < c) {
+    const int ci = ci0 + j;
+    for (int k = k0; k < k1; ++k) {
+      const double v = mode == 1 ? conv_v(db, vt, cout, k / 9, k % 9) : (mode == 2 ? (double)vt[k] : (double)db[k]);
+      const size_t idx = (size_t)k * cin_tot + ci;
       const double wv = w[idx];
       swv += wv * v;
       swr += wv * raw[idx];
     }
-  part[j] = (float)swv;
-  part[c + j] = (float)(inv[j] * (swr - (double)mean[j] * swv));
+  }
+  __shared__ double red[2][256];
+  red[0][threadIdx.x] = swv;
+  red[1][threadIdx.x] = swr;
+  __syncthreads();
+  if (sub == 0 && j < c) {
+    swv = ((red[0][cl] + red[0][cl + 64]) + red[0][cl + 128]) + red[0][cl + 192];
+    swr = ((red[1][cl] + red[1][cl + 64]) + red[1][cl + 128]) + red[1][cl + 192];
+    float* o = part + (size_t)blockIdx.y * 2 * c;
+    o[j] = (float)swv;
+    o[c + j] = (float)(inv[j] * (swr - (double)mean[j] * swv));
+  }
 }
 
 extern "C" int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* raw, int cout, int cin_tot,
@@ -1135,66 +1253,8 @@ extern "C" int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* r
   CNN_REQUIRE(mode >= 1 && mode <= 3 && ci0 >= 0 && ci0 + c <= cin_tot && (mode == 2 || db),
               "bn_consumer_sums: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_consumer_sums_kernel, dim3((c + 63) / 64), dim3(64), 0, s, mode, w, raw, cout,
-                     cin_tot, ci0, c, db, vtab, mean, invstd, part);
+  hipLaunchKernelGGL(bn_consumer_sums_kernel, dim3((c + 63) / 64, CNNITMO_CONSUMER_ROWS), dim3(256), 0, s,
+                     mode, w, raw, cout, cin_tot, ci0, c, db, vtab, mean, invstd, part);
   return cnnitmo_check_launch("bn_consumer_sums");
 }
 
-// The MaxPooling2D share of the same sums for a pooled BN output: the pool routes
-// dy_pool[p] to the argmax pixel of window p, so it adds sum_p dy_pool[p] and
-// sum_p dy_pool[p] * rhat[argmax(p)] (r read at the argmax only).
-// part rows: cnnitmo_bn_bwd_rows(p_pool, c).
-template <typename T>
-__global__ void pool_bnsums_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ idx, int H, int W,
-                                   long Pp, int C, const T* __restrict__ r, long r_ld, int r_off,
-                                   const float* __restrict__ mean, const float* __restrict__ inv,
-                                   float* __restrict__ part) {
-  constexpr int VE = Vec16<T>::N;
-  const int tpp = C / VE, rows = 256 / tpp;
-  const int tid = threadIdx.x;
-  const int row = tid / tpp, cv = tid - row * tpp, c0 = cv * VE;
-  const int Ho = H / 2, Wo = W / 2;
-  float acc[2][VE];
-  float mu[VE], is[VE];
-#pragma unroll
-  for (int e = 0; e < VE; ++e) {
-    acc[0][e] = acc[1][e] = 0.f;
-    mu[e] = row < rows ? mean[c0 + e] : 0.f;
-    is[e] = row < rows ? inv[c0 + e] : 0.f;
-  }
-  if (row < rows) {
-    for (long po = (long)blockIdx.x * rows + row; po < Pp; po += (long)gridDim.x * rows) {
-      const int n = (int)(po / ((long)Ho * Wo));
-      const int rem = (int)(po - (long)n * Ho * Wo);
-      const int ho = rem / Wo, wo = rem - ho * Wo;
-      float g[VE];
-      Pack16<T>::load(dy + (size_t)po * C + c0, g);
-#pragma unroll
-      for (int e = 0; e < VE; ++e) {
-        const int k = idx[(size_t)po * C + c0 + e];
-        const long pin = ((long)n * H + 2 * ho + (k >> 1)) * W + 2 * wo + (k & 1);
-        const float rv = to_f32(r[(size_t)pin * r_ld + r_off + c0 + e]);
-        acc[0][e] += g[e];
-        acc[1][e] += g[e] * (rv - mu[e]) * is[e];
-      }
-    }
-  }
-  block_reduce_rows<VE, 2>(acc, C, part);
-}
-
-extern "C" int cnnitmo_pool_bnsums(int dtype, const void* dy, const uint8_t* idx, int n, int h, int w,
-                                   int c, const void* r, int r_ld, int r_off, const float* mean,
-                                   const float* invstd, float* part, void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  const long Pp = (long)n * (h / 2) * (w / 2);
-  const int G = cnnitmo_bn_bwd_rows(Pp, c);
-  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
-  CNN_REQUIRE(c % VE == 0 && c / VE <= 256, "pool_bnsums: unsupported channel count %d", c);
-  if (dtype == CNNITMO_BF16)
-    hipLaunchKernelGGL(pool_bnsums_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dy, idx, h, w, Pp, c,
-                       (const bf16*)r, (long)r_ld, r_off, mean, invstd, part);
-  else
-    hipLaunchKernelGGL(pool_bnsums_kernel<float>, dim3(G), dim3(256), 0, s, (const float*)dy, idx, h, w, Pp, c,
-                       (const float*)r, (long)r_ld, r_off, mean, invstd, part);
-  return cnnitmo_check_launch("pool_bnsums");
-}

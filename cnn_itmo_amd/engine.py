@@ -60,6 +60,7 @@ class Value:
         self.producer = None  # BlockStage writing this value
         self.sum_consumers = 0  # >0: BN-backward sums come from this many consumers (no reduce pass)
         self.bn_contrib = []  # per-step partial-sum tensors [rows][2][c] from the consumers
+        self.pool_route = None  # (pooled gradient, argmax idx): a deferred MaxPooling2D backward
         self.cs = None  # coefficient buffers of the owner (persist across steps)
         self.ch = None
 
@@ -111,6 +112,8 @@ class Value:
         self.buf = None
         self.gbuf = None
         self.ginit = False
+        self.bn_contrib = []
+        self.pool_route = None
 
 
 class Stage:
@@ -290,6 +293,9 @@ class BlockStage(Stage):
                 part = torch.cat(v.bn_contrib)
                 prow = part.numel() // (2 * cout)
             else:
+                if v.pool_route is not None:  # route the deferred pool gradient before the reduce
+                    ops.maxpool_bwd(e.dt, v.pool_route[0], v.pool_route[1], dy)
+                    v.pool_route = None
                 part = torch.empty(rows * 2 * cout, device=e.device, dtype=torch.float32)
                 ops.bn_bwd_reduce(e.dt, dy, self.r, cout, self.smean, self.sinv, flags, e.drop_seed,
                                   self.drop_id, part)
@@ -298,7 +304,13 @@ class BlockStage(Stage):
             coef = torch.empty(3 * cout, device=e.device, dtype=torch.float32)
             ops.bn_bwd_finalize(part, prow, cout, P, e.p(bn.name + "/gamma"), self.smean, self.sinv,
                                 e.g(bn.name + "/gamma"), e.g(bn.name + "/beta"), coef)
-            ops.bn_bwd_apply(e.dt, dy, self.r, cout, coef, flags, e.drop_seed, self.drop_id, dz, part2)
+            if v.pool_route is not None:
+                assert not flags, "pool routing with dropout/parity"
+                ops.bn_bwd_apply_pooled(e.dt, dy, self.r, cout, coef, v.pool_route[0], v.pool_route[1], dz,
+                                        part2)
+                v.pool_route = None
+            else:
+                ops.bn_bwd_apply(e.dt, dy, self.r, cout, coef, flags, e.drop_seed, self.drop_id, dz, part2)
         else:
             ops.bn_bwd_apply(e.dt, dy, self.r, cout, None, flags | L.NO_BN, e.drop_seed,
                              self.drop_id, dz, part2)
@@ -332,7 +344,7 @@ class BlockStage(Stage):
                     fold = self.vin.coef() + (db, bsum)
                 ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
                 for m, ci0 in targets:
-                    pm = torch.empty(2 * m.c, device=e.device, dtype=torch.float32)
+                    pm = torch.empty(L.CONSUMER_ROWS * 2 * m.c, device=e.device, dtype=torch.float32)
                     ops.bn_consumer_sums(1, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, db,
                                          bsum, m.producer.smean, m.producer.sinv, pm)
                     m.bn_contrib.append(pm)
@@ -340,7 +352,7 @@ class BlockStage(Stage):
                 fold = self.vin.coef() + (psum,) if par else None
                 ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
                 for m, ci0 in targets:
-                    pm = torch.empty(2 * m.c, device=e.device, dtype=torch.float32)
+                    pm = torch.empty(L.CONSUMER_ROWS * 2 * m.c, device=e.device, dtype=torch.float32)
                     ops.bn_consumer_sums(2, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, None,
                                          psum, m.producer.smean, m.producer.sinv, pm)
                     m.bn_contrib.append(pm)
@@ -380,18 +392,22 @@ class PoolStage(Stage):
         e = self.eng
         if not self.vin.needs_grad:
             return
-        if not self.vin.ginit:
-            if self.vin.place:
-                raise NotImplementedError("pool gradient into an uninitialised concat slice")
-            self.vin.ensure_grad(n, e.tdtype, e.device, zero=True)
         v = self.vin
-        if v.sum_consumers:  # this pool's share of the BN-backward sums of its input
+        if v.sum_consumers and v.ginit:
+            # this pool's share of the BN-backward sums of its input; the routing itself is
+            # deferred into the producer's BN apply (cnnitmo_bn_bwd_apply_pooled)
             pp = n * (v.h // 2) * (v.w // 2)
             rows = ops.bn_bwd_rows(pp, v.c)
             pm = torch.empty(rows * 2 * v.c, device=e.device, dtype=torch.float32)
             ops.pool_bnsums(e.dt, self.vout.gbuf, self.idx, v.view(n), v.producer.smean, v.producer.sinv, pm)
             v.bn_contrib.append(pm)
-        ops.maxpool_bwd(e.dt, self.vout.gbuf, self.idx, self.vin.gview(n))
+            v.pool_route = (self.vout.gbuf, self.idx)
+        else:
+            if not v.ginit:
+                if v.place:
+                    raise NotImplementedError("pool gradient into an uninitialised concat slice")
+                v.ensure_grad(n, e.tdtype, e.device, zero=True)
+            ops.maxpool_bwd(e.dt, self.vout.gbuf, self.idx, v.gview(n))
         self.idx = None
 
 
@@ -432,7 +448,7 @@ class HeadStage(Stage):
         ops.head_finalize(part, rows, self.cin, n * e.h_valid * self.vin.w * 3, loss_acc,
                           e.g(self.name + "/kernel"), e.g(self.name + "/bias"), aff, raw=raw)
         if raw is not None:
-            pm = torch.empty(2 * v.c, device=e.device, dtype=torch.float32)
+            pm = torch.empty(L.CONSUMER_ROWS * 2 * v.c, device=e.device, dtype=torch.float32)
             ops.bn_consumer_sums(3, e.p(self.name + "/kernel"), raw, 3, self.cin, 0, v.c, e.g(self.name + "/bias"),
                                  None, v.producer.smean, v.producer.sinv, pm)
             v.bn_contrib.append(pm)
@@ -547,7 +563,7 @@ def _plan_bn_sums(stages):
     """Mark the folded BN outputs whose backward sums (sum dy, sum dy*rhat) can be
     assembled from their consumers instead of a pass over dy: every consumer must be a
     conv3x3 / tconv / head (cnnitmo_bn_consumer_sums) or a MaxPooling2D
-    (cnnitmo_pool_bnsums).  Dropout outputs are materialised, hence never folded."""
+    (cnnitmo_maxpool2x2_bwd_bnsums).  Dropout outputs are materialised, hence never folded."""
     readers = {}
     for st in stages:
         srcs = []

@@ -221,6 +221,13 @@ def bn_bwd_apply(dt, dy: View, r, c, coef, flags, seed, layer, dz, part):
          seed, layer, dy.h, dy.w, ptr(dz), ptr(part), stream_ptr())
 
 
+def bn_bwd_apply_pooled(dt, dy: View, r, c, coef, dyp, idx, dz, part):
+    """bn_bwd_apply with a deferred MaxPooling2D backward folded in: dy += dyp routed by idx."""
+    rp, rld, roff = _rview(r, c)
+    call("cnnitmo_bn_bwd_apply_pooled", dt, dy.ptr, dy.ld, dy.off, rp, rld, roff, dy.n, dy.h, dy.w, c,
+         ptr(coef), ptr(dyp), ptr(idx), ptr(dz), ptr(part), stream_ptr())
+
+
 def colsum(part, rows, cols, groups, out):
     ws = reduce_ws(rows, cols, part.device)
     call("cnnitmo_colsum", ptr(part), rows, cols, groups, ptr(out), ws.data_ptr(), stream_ptr())
@@ -251,16 +258,17 @@ def head_finalize(part, rows, cin, numel, loss_acc, dw, db, aff=None, raw=None):
 
 
 def bn_consumer_sums(mode, w, raw, cout, cin_tot, ci0, c, db, vtab, mean, inv, part):
-    """part[2][c] = (sum dy, sum dy*rhat) of a BN output from its consumer's weight
+    """part[CONSUMER_ROWS][2][c] = (sum dy, sum dy*rhat) of a BN output from its consumer's weight
     gradient (mode 1 conv3x3, 2 tconv, 3 head); see cnn_itmo.h."""
     call("cnnitmo_bn_consumer_sums", mode, ptr(w), ptr(raw), cout, cin_tot, ci0, c, ptr(db), ptr(vtab),
          ptr(mean), ptr(inv), ptr(part), stream_ptr())
 
 
-def pool_bnsums(dt, dy, idx, vin: View, mean, inv, part):
-    """The MaxPooling2D share of those sums (rows = bn_bwd_rows(pooled pixels, c))."""
-    call("cnnitmo_pool_bnsums", dt, ptr(dy), ptr(idx), vin.n, vin.h, vin.w, vin.c, vin.ptr, vin.ld, vin.off,
-         ptr(mean), ptr(inv), ptr(part), stream_ptr())
+def pool_bnsums(dt, dyp, idx, r: View, mean, inv, part):
+    """The MaxPooling2D share of a folded BN output's backward sums (rows =
+    bn_bwd_rows(pooled pixels, c)); r is the pool input's view."""
+    call("cnnitmo_pool_bnsums", dt, ptr(dyp), ptr(idx), r.n, r.h, r.w, r.c, r.ptr, r.ld, r.off, ptr(mean),
+         ptr(inv), ptr(part), stream_ptr())
 
 
 def rmsprop(p, g, a, lr, rho, eps, grad_scale=1.0):

@@ -239,6 +239,13 @@ int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off, const
                          void* stream);
 /* r view: (r_ld, r_off).  part columns: [c], or [4][c] by pixel parity with
  * CNNITMO_PARITY (h, w = the spatial size, needed only then). */
+/* The same for a BN output that also feeds a MaxPooling2D whose backward was
+ * deferred: dy += the pool gradient dy_pool [n][h/2][w/2][c] routed by idx to
+ * this pixel (replaces cnnitmo_maxpool2x2_bwd + the dy read-modify-write). */
+int cnnitmo_bn_bwd_apply_pooled(int dtype, const void* dy, int dy_ld, int dy_off, const void* r,
+                                int r_ld, int r_off, int n, int h, int w, int c, const float* coef,
+                                const void* dy_pool, const uint8_t* idx, void* dz, float* part,
+                                void* stream);
 /* BN-backward sums WITHOUT a pass over dy: for a BN output whose gradient is the
  * input-gradient of a linear consumer (mode 1 conv3x3, 2 tconv2x2, 3 the 1x1
  * head), part[2][c] = {sum dy, sum dy*rhat} over the consumer's input channels
@@ -246,12 +253,14 @@ int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy_off, const
  * the *_wgrad / head_finalize call) and V (mode 1: db[cout] + border sums
  * vtab[8][cout]; mode 2: parity sums vtab[4*cout]; mode 3: db[3]).  Exact: the
  * dgrad is the transpose of the same map.  Feed to cnnitmo_bn_bwd_finalize.
- * cnnitmo_pool_bnsums adds a MaxPooling2D consumer's share (rows =
- * cnnitmo_bn_bwd_rows(n*(h/2)*(w/2), c)); r is the pooled tensor's view. */
+ * part has CNNITMO_CONSUMER_ROWS rows [rows][2][c].  cnnitmo_pool_bnsums adds a
+ * MaxPooling2D consumer's share (dyp: the pooled gradient; r: the pool input's
+ * view; rows = cnnitmo_bn_bwd_rows(n*(h/2)*(w/2), c)). */
+#define CNNITMO_CONSUMER_ROWS 16
 int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* raw, int cout, int cin_tot, int ci0,
                              int c, const float* db, const float* vtab, const float* mean,
                              const float* invstd, float* part, void* stream);
-int cnnitmo_pool_bnsums(int dtype, const void* dy, const uint8_t* idx, int n, int h, int w, int c,
+int cnnitmo_pool_bnsums(int dtype, const void* dyp, const uint8_t* idx, int n, int h, int w, int c,
                         const void* r, int r_ld, int r_off, const float* mean, const float* invstd,
                         float* part, void* stream);
 /* Column sums of partial rows -> out[groups-folded c] (fp32, written). */

@@ -193,3 +193,58 @@ def test_head_folded(dt):
     close(host(dw) * 1e3, dz.reshape(-1, 3).T @ y.reshape(-1, C) * 1e3, "f32", "head dw")
     close(host(db) * 1e3, dz.reshape(-1, 3).sum(0) * 1e3, "f32", "head db")
     close(host(dx).reshape(dx_ref.shape) * 1e3, dx_ref * 1e3, dt, "head dx")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("H,W", [(6, 10), (7, 9)])
+def test_pool_deferred_route_and_sums(dt, H, W):
+    """A pooled folded BN output: the pool's share of the BN-backward sums
+    (cnnitmo_pool_bnsums) and the BN apply with the pool routing folded in
+    (cnnitmo_bn_bwd_apply_pooled) == maxpool_bwd followed by bn_bwd_apply."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(14)
+    N, C, ld, off = 2, 64, 96, 32
+    Ho, Wo = H // 2, W // 2
+    d = DT[dt]
+    rb = np.maximum(rng.standard_normal((N, H, W, ld)), 0).astype(np.float32)
+    dy = rng.standard_normal((N, H, W, C)).astype(np.float32)
+    dyp = rng.standard_normal((N, Ho, Wo, C)).astype(np.float32)
+    idx = rng.integers(0, 4, (N, Ho, Wo, C)).astype(np.uint8)
+    mean = rng.uniform(0.2, 0.8, C).astype(np.float32)
+    inv = rng.uniform(0.5, 2.0, C).astype(np.float32)
+    coef = rng.standard_normal(3 * C).astype(np.float32)
+    P = N * H * W
+    rv = ops.View(dev(rb, dt).reshape(-1), N, H, W, C, ld, off)
+    dyp_t, idx_t = dev(dyp, dt).reshape(-1), torch.tensor(idx.reshape(-1)).cuda()
+
+    rows = ops.bn_bwd_rows(N * Ho * Wo, C)
+    pm = torch.empty(rows, 2, C, device="cuda")
+    ops.pool_bnsums(d, dyp_t, idx_t, rv, cu(mean), cu(inv), pm)
+    sums = torch.empty(2, C, device="cuda")
+    ops.colsum(pm, rows, 2 * C, 1, sums)
+    r64 = rnd(rb, dt)[..., off:].astype(np.float64)
+    g64 = rnd(dyp, dt).astype(np.float64)
+    rwin = r64[:, :2 * Ho, :2 * Wo].reshape(N, Ho, 2, Wo, 2, C).transpose(0, 1, 3, 2, 4, 5).reshape(N, Ho, Wo, 4, C)
+    rarg = np.take_along_axis(rwin, idx[:, :, :, None, :].astype(np.int64), axis=3)[:, :, :, 0]
+    want = np.stack([g64.sum((0, 1, 2)), (g64 * (rarg - mean) * inv).sum((0, 1, 2))])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(host(sums), want, rtol=1e-4, atol=1e-3)
+
+    rows2 = ops.bn_bwd_rows(P, C)
+    dy_a = dev(dy, dt).reshape(-1)
+    dz_a = torch.empty(P * C, dtype=TDT[dt], device="cuda")
+    pa = torch.empty(rows2, C, device="cuda")
+    ops.bn_bwd_apply_pooled(d, ops.View(dy_a, N, H, W, C, C), rv, C, cu(coef), dyp_t, idx_t, dz_a, pa)
+    dy_b = dev(dy, dt).reshape(-1)
+    ops.maxpool_bwd(d, dyp_t, idx_t, ops.View(dy_b, N, H, W, C, C))
+    dz_b = torch.empty(P * C, dtype=TDT[dt], device="cuda")
+    pb = torch.empty(rows2, C, device="cuda")
+    ops.bn_bwd_apply(d, ops.View(dy_b, N, H, W, C, C), rv, C, cu(coef), 0, 0, 0, dz_b, pb)
+    db_a, db_b = torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+    ops.colsum(pa, rows2, C, 1, db_a)
+    ops.colsum(pb, rows2, C, 1, db_b)
+    torch.cuda.synchronize()
+    # bf16: the reference path rounds dy + routed to bf16 before the apply
+    tol = 1e-5 if dt == "f32" else 2e-2
+    np.testing.assert_allclose(host(dz_a), host(dz_b), rtol=tol, atol=tol * 4)
+    np.testing.assert_allclose(host(db_a), host(db_b), rtol=tol, atol=tol * 20)
