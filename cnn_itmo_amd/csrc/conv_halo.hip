@@ -68,7 +68,7 @@ __device__ __forceinline__ int hswz(int row, int piece) {
 //   MODE 1: Conv2DTranspose(2, s2) forward: a 1x1 GEMM over the input pixels
 //           (TH x TW patch, no halo) whose column n = tap*cout + co is scattered
 //           to output pixel (2y + tap/2, 2x + tap%2)
-template <int MODE, int TH, int TW, int BN, int ST>
+template <int MODE, int TH, int TW, int BN, int ST, int EPI = 0>
 struct HaloCfg {
   static constexpr int NWAVE = TH <= 8 ? TH : 8, NT = NWAVE * 64;
   static constexpr int RPW = TH / NWAVE;  // tile rows per wave
@@ -83,10 +83,12 @@ struct HaloCfg {
   static constexpr int STAGE = PATCH + B_INSTR * 1024;
   static constexpr int CLD = BN + 8;  // C staging row (bf16), per wave TW rows
   static constexpr int C_BYTES = NWAVE * RPW * TW * CLD * 2;
+  // cross-wave partial sums: [NWAVE][BN][2] (BN stats) or [NWAVE][BN][4] (EPI 1 parity sums)
+  static constexpr int RED_BYTES = NWAVE * BN * (EPI ? 16 : 8);
   // the epilogue stages C in the stage it just consumed when it fits, else in its own region
-  static constexpr bool C_IN_STAGE = C_BYTES + NWAVE * BN * 8 <= STAGE;
+  static constexpr bool C_IN_STAGE = C_BYTES + RED_BYTES <= STAGE;
   static constexpr int C_OFF = ST * STAGE;
-  static constexpr int SMEM = ST * STAGE + (C_IN_STAGE ? 0 : C_BYTES + NWAVE * BN * 8);
+  static constexpr int SMEM = ST * STAGE + (C_IN_STAGE ? 0 : C_BYTES + RED_BYTES);
   static constexpr int SG = TH * TW / 256;  // BN-partial-sum rows per tile (256 pixels each)
   static_assert(TH * TW % 256 == 0 && TW % 16 == 0, "tile");
 };
@@ -99,15 +101,18 @@ struct HaloArgs {
   int nchunks;           // cin / 32
 };
 
-template <int MODE, int TH, int TW, int BN, int ST>
-__global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm_kernel(const HaloArgs h) {
-  using C = HaloCfg<MODE, TH, TW, BN, ST>;
+// EPI 1 (MODE 0 dgrad only): the producer's BN backward fused into the store, see
+// FwdArgs::bnb_* and epilogue_bnb below.
+template <int MODE, int TH, int TW, int BN, int ST, int EPI>
+__global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo_gemm_kernel(const HaloArgs h) {
+  using C = HaloCfg<MODE, TH, TW, BN, ST, EPI>;
   constexpr int KT = C::KT;
   static_assert(C::SMEM <= 160 * 1024, "LDS");
   constexpr int NWAVE = C::NWAVE, FM = C::FM, FN = C::FN, STAGE = C::STAGE, PW = C::PW;
   constexpr int RPW = C::RPW, FMR = C::FMR;
   constexpr int NPI = C::NPI, NBI = C::NBI;
   constexpr int CPR = BN / 8;  // 16-byte output pieces per pixel
+  constexpr int CPRP = CPR <= 4 ? 4 : (CPR <= 8 ? 8 : 16);  // EPI 1: lanes per pixel (power of 2)
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -329,6 +334,145 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm
     zero_acc();
   };
 
+  // EPI 1: dgrad output columns [bnb_c0, bnb_c1) are the gradient g of a folded BN
+  // output whose backward coefficients are known (consumer-derived sums): store
+  // dz = [r>0]*(a*g - b*r + e) of the bf16-rounded g (as cnnitmo_bn_bwd_apply does)
+  // into bnb_out and its column sums (by pixel parity) into stats rows; the other
+  // columns are stored as g.  Works in the 16-byte piece layout of the store loop:
+  // lane l always owns piece column cc = l % CPRP and pixel-column parity
+  // (l / CPRP) & 1 (CPRP = CPR rounded up to a power of 2, x0 even); the pixel-row parity of its i-th piece
+  // is compile-time (y0, oh0 even).  The r pieces are loaded first and waited for
+  // with vmcnt(0) after the C tile is staged (that also retires the in-flight
+  // prefetch of the next item).
+  static_assert(EPI == 0 || (MODE == 0 && TH % 2 == 0 && TW % 2 == 0 && RPW % 2 == 0), "EPI 1 layout");
+  constexpr int NPC = EPI ? RPW * TW * CPRP / 64 : 1;  // pieces per lane (lanes with cc >= CPR idle)
+  constexpr int PXS = 64 / CPRP;                       // pixel step between a lane's pieces
+  static_assert(EPI == 0 || TW % PXS == 0, "row parity per piece");
+  // r pieces and coefficients of the item being stored
+  uint4 rv[NPC];
+  float ca[8], cb[8], ce[8];
+  auto bnb_prefetch = [&](const Pos& e) {
+    const int x0 = e.x0, oh0 = e.y0 + wave * RPW;
+    const int cc = lane % CPRP, n = e.nb * BN + cc * 8;
+    const int c0 = p.bnb_c0, cbn = p.bnb_c1 - p.bnb_c0;
+    const bool fz = cc < CPR && n >= c0 && n < p.bnb_c1;
+    const int nz = fz ? n - c0 : 0;
+    const bf16* __restrict__ R = (const bf16*)p.bnb_r;
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) {
+      const int px = lane / CPRP + PXS * i;
+      const int rr = px / TW, col = px - rr * TW, oh = oh0 + rr;
+      const bool ok = fz && oh < p.ho && x0 + col < p.wo;
+      const long m = ((long)e.img * p.ho + oh) * p.wo + x0 + col;
+      rv[i] = *reinterpret_cast<const uint4*>(ok ? (const void*)(R + (size_t)m * p.bnb_r_ld + p.bnb_r_off + nz)
+                                                 : (const void*)h_zero_page);
+    }
+    const float* cp = p.bnb_coef + nz;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ca[k] = fz ? cp[k] : 0.f;
+      cb[k] = fz ? cp[cbn + k] : 0.f;
+      ce[k] = fz ? cp[2 * cbn + k] : 0.f;
+    }
+  };
+  auto epilogue_bnb = [&](const Pos& e, int buf) {
+    bnb_prefetch(e);  // (issuing these before the item's last compute measured slower)
+    const int img = e.img, y0 = e.y0, x0 = e.x0;
+    const int n0 = e.nb * BN;
+    const int oh0 = y0 + wave * RPW;
+    char* cbase = C::C_IN_STAGE ? smem + buf * STAGE : smem + C::C_OFF;
+    bf16* Cs = reinterpret_cast<bf16*>(cbase) + wave * RPW * TW * C::CLD;
+    float* red = reinterpret_cast<float*>(cbase + C::C_BYTES);  // [NWAVE][BN][4]
+    const int cc = lane % CPRP, n = n0 + cc * 8;
+    const bool on = cc < CPR;  // BN = 48: 6 of every 8 lanes
+    const int c0 = p.bnb_c0, cbn = p.bnb_c1 - p.bnb_c0;
+    const bool fz = on && n >= c0 && n < p.bnb_c1;
+    const int nz = fz ? n - c0 : 0;
+    // g -> LDS (bf16) in the MFMA layout
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = f / FMR, col = (f % FMR) * 16 + (lane >> 4) * 4 + r;
+          Cs[(rr * TW + col) * C::CLD + j * 16 + (lane & 15)] = from_f32<bf16>(acc[f][j][r]);
+        }
+    __syncthreads();
+    wait_vm<0>();
+    float sm[2][8];  // [pixel-row parity][channel] sums of this lane's (column-parity) pixels
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sm[0][k] = sm[1][k] = 0.f;
+    bf16* __restrict__ O = (bf16*)p.out;
+    bf16* __restrict__ Z = (bf16*)p.bnb_out;
+#pragma unroll
+    for (int i = 0; i < NPC; ++i) {
+      const int px = lane / CPRP + PXS * i;
+      const int rr = px / TW, col = px - rr * TW, oh = oh0 + rr;
+      const int rp = ((PXS * i) / TW) & 1;  // compile-time row parity of this piece
+      const bool valid = on && oh < p.ho && x0 + col < p.wo;
+      const long m = ((long)img * p.ho + oh) * p.wo + x0 + col;
+      uint4 v = *reinterpret_cast<const uint4*>(Cs + px * C::CLD + (on ? cc : 0) * 8);
+      if (fz) {
+        const bf16* gv = reinterpret_cast<const bf16*>(&v);
+        const bf16* rq = reinterpret_cast<const bf16*>(&rv[i]);
+        uint4 o;
+        bf16* ov = reinterpret_cast<bf16*>(&o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float g = to_f32(gv[k]), r = to_f32(rq[k]);
+          const bf16 d = from_f32<bf16>(r > 0.f ? ca[k] * g - cb[k] * r + ce[k] : 0.f);
+          ov[k] = d;
+          sm[rp][k] += valid ? to_f32(d) : 0.f;
+        }
+        v = o;
+      }
+      uint4* dst = !valid ? h_sink + lane
+                   : fz   ? reinterpret_cast<uint4*>(Z + (size_t)m * cbn + nz)
+                          : reinterpret_cast<uint4*>(O + (size_t)m * p.out_ld + p.out_off + n);
+      *dst = v;
+    }
+    // lanes sharing (cc, column parity) differ in lane bits >= log2(2*CPRP)
+#pragma unroll
+    for (int o = 2 * CPRP; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sm[0][k] += __shfl_xor(sm[0][k], o, 64);
+        sm[1][k] += __shfl_xor(sm[1][k], o, 64);
+      }
+    if (lane < 2 * CPRP && on) {
+      const int cp = lane / CPRP;  // pixel-column parity
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[(wave * BN + cc * 8 + k) * 4 + 0 * 2 + cp] = sm[0][k];
+        red[(wave * BN + cc * 8 + k) * 4 + 1 * 2 + cp] = sm[1][k];
+      }
+    }
+    __syncthreads();
+    if (tid < C::SG * BN) {
+      const int g = tid / BN, col = tid - g * BN;
+      const int nn = n0 + col;
+      constexpr int WPG = NWAVE / C::SG;
+      if (nn >= c0 && nn < p.bnb_c1) {
+        float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int w = 0; w < WPG; ++w)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) t[k] += red[((g * WPG + w) * BN + col) * 4 + k];
+        const long tile = ((long)img * h.tiles_y + y0 / TH) * h.tiles_x + x0 / TW;
+        const long row = tile * C::SG + g;
+        if (p.bnb_par) {
+          float* st = p.stats + (size_t)row * 4 * cbn + (nn - c0);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) st[(size_t)k * cbn] = t[k];
+        } else {
+          p.stats[(size_t)row * cbn + (nn - c0)] = (t[0] + t[1]) + (t[2] + t[3]);
+        }
+      }
+    }
+    zero_acc();
+  };
+
   // ST-stage ring over items.  vmcnt retires in issue order and counts the
   // epilogue's global stores too, so the wave tracks how many vector-memory ops
   // it issued after the loads of the item it is about to consume and waits for
@@ -336,10 +480,12 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm
   // count is a lower bound for waves whose stats stores were exec-masked off,
   // which only makes their wait stricter.
   constexpr int L = NPI + NBI;
-  constexpr int NST = (RPW * TW * CPR + 63) / 64;  // output store instructions per wave
+  // output store instructions per wave
+  constexpr int NST = EPI ? RPW * TW * CPRP / 64 : (RPW * TW * CPR + 63) / 64;
   static_assert(RPW * TW * CPR % 64 == 0, "every lane issues the same number of stores");
   // BN partial sums are stored by threads tid < SG*BN: waves 0 .. (SG*BN-1)/64
-  const int S = NST + ((stats && wave * 64 < C::SG * BN) ? 2 : 0);
+  // EPI 1: the sums stores are not counted (an undercount only makes a wait stricter)
+  const int S = NST + ((!EPI && stats && wave * 64 < C::SG * BN) ? 2 : 0);
   Pos ep = ip;  // position of the item being computed
   int issued = 0;
   int mq[ST];  // mq[k]: value of `issued` right after the loads of item t+k
@@ -369,7 +515,8 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm
     compute(buf);
     if (ep.ch == nch - 1) {
       __syncthreads();  // every wave is done reading this stage: reuse it for the C tile
-      epilogue(ep, buf);
+      if constexpr (EPI == 1) epilogue_bnb(ep, buf);
+      else epilogue(ep, buf);
       issued += S;
     }
     step(ep);
@@ -379,16 +526,17 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST>::NT)) void halo_gemm
   }
 }
 
-template <int MODE, int TH, int TW, int BN>
+template <int MODE, int TH, int TW, int BN, int EPI = 0>
 void launch_cfg(const HaloArgs& h, hipStream_t s) {
   // one workgroup per CU (LDS-limited); as many ring stages as fit in 160 KB
   const dim3 grid((unsigned)((h.npairs + h.per_block - 1) / h.per_block));
-  if constexpr (HaloCfg<MODE, TH, TW, BN, 5>::SMEM <= 160 * 1024)
-    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 5>), grid, dim3((HaloCfg<MODE, TH, TW, BN, 2>::NT)), 0, s, h);
-  else if constexpr (HaloCfg<MODE, TH, TW, BN, 3>::SMEM <= 160 * 1024)
-    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 3>), grid, dim3((HaloCfg<MODE, TH, TW, BN, 2>::NT)), 0, s, h);
+  const dim3 block((HaloCfg<MODE, TH, TW, BN, 2, EPI>::NT));
+  if constexpr (HaloCfg<MODE, TH, TW, BN, 5, EPI>::SMEM <= 160 * 1024)
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 5, EPI>), grid, block, 0, s, h);
+  else if constexpr (HaloCfg<MODE, TH, TW, BN, 3, EPI>::SMEM <= 160 * 1024)
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 3, EPI>), grid, block, 0, s, h);
   else
-    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 2>), grid, dim3((HaloCfg<MODE, TH, TW, BN, 2>::NT)), 0, s, h);
+    hipLaunchKernelGGL((halo_gemm_kernel<MODE, TH, TW, BN, 2, EPI>), grid, block, 0, s, h);
 }
 
 int halo_cfg_env() {
@@ -400,7 +548,7 @@ int halo_cfg_env() {
 }
 
 struct HaloPlan {
-  int mode, bn, th, tw;
+  int mode, bn, th, tw, epi;
 };
 
 // mode 0: conv3x3 stride 1 ('same'); mode 1: tconv2x2 s2 forward (pixel scatter)
@@ -411,6 +559,19 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
   }();
   if (!en) return false;
   if (a.cin % 32 || a.a_ld % 8 || a.a_off % 8 || a.out_ld % 8 || a.out_off % 8) return false;
+  pl.epi = 0;
+  if (a.bnb_out) {  // fused BN backward: conv3x3 dgrad, 16x32 tiles, BN 64 / 32
+    if (a.ntaps != 9 || a.scale != 1 || a.scatter || a.hs != a.ho || a.ws != a.wo) return false;
+    if (a.bnb_c0 % 8 || a.bnb_c1 % 8 || a.bnb_c0 < 0 || a.bnb_c1 > a.N || a.bnb_c0 >= a.bnb_c1 ||
+        a.bnb_r_ld % 8 || a.bnb_r_off % 8)
+      return false;
+    pl.mode = 0;
+    pl.epi = 1;
+    pl.bn = a.N % 64 == 0 ? 64 : (a.N % 48 == 0 ? 48 : (a.N % 32 == 0 ? 32 : 0));
+    pl.th = 16;
+    pl.tw = 32;
+    return pl.bn != 0;
+  }
   if (a.ntaps == 9 && a.scale == 1 && !a.scatter && a.hs == a.ho && a.ws == a.wo) {
     pl.mode = 0;
     static const int force = [] {
@@ -469,7 +630,11 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
   }
   h.per_block = (h.npairs + ncu - 1) / ncu;
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
-  if (pl.mode == 1) {
+  if (pl.epi == 1) {
+    if (pl.bn == 64) launch_cfg<0, 16, 32, 64, 1>(h, s);
+    else if (pl.bn == 48) launch_cfg<0, 16, 32, 48, 1>(h, s);
+    else launch_cfg<0, 16, 32, 32, 1>(h, s);
+  } else if (pl.mode == 1) {
     if (pl.bn == 128) launch_cfg<1, 8, 32, 128>(h, s);
     else launch_cfg<1, 8, 32, 64>(h, s);
   } else if (pl.th == 4) {
@@ -494,7 +659,8 @@ const char* halo_name(const FwdArgs& a) {
   HaloPlan pl;
   if (!halo_plan(a, pl)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "halo_gemm_kernel<%d,%d,%d,%d>", pl.mode, pl.th, pl.tw, pl.bn);
+  snprintf(buf, sizeof(buf), "halo_gemm_kernel<%d,%d,%d,%d%s>", pl.mode, pl.th, pl.tw, pl.bn,
+           pl.epi ? ",bnb" : "");
   return buf;
 }
 

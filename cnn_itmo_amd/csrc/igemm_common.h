@@ -27,6 +27,15 @@ struct FwdArgs {
   float* stats;  // [mblocks][2][N]
   int mblocks, nblocks;
   const float* border;  // folded-BN zero-padding correction [cout][8] (conv3x3 fwd), or null
+  // conv3x3 dgrad with the producer's BN backward fused (halo kernel only): output
+  // columns [bnb_c0, bnb_c1) become dz = [r>0]*(a*g - b*r + e) -> bnb_out [M][c1-c0],
+  // with partial sums of dz -> stats [rows][bnb_par ? 4 : 1][c1-c0]
+  int bnb_c0, bnb_c1, bnb_par;
+  const float* bnb_coef;  // [3][c1-c0]
+  const void* bnb_r;
+  long bnb_r_ld;
+  int bnb_r_off;
+  void* bnb_out;
 };
 
 // Out-of-bounds-tap correction for a folded BN shift (see cnnitmo_fold_conv3x3):

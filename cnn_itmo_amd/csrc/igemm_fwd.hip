@@ -445,6 +445,43 @@ extern "C" int cnnitmo_conv3x3_dgrad(int dtype, const void* dz, int n, int h, in
   return dispatch(dtype, a, stream, "conv3x3_dgrad");
 }
 
+namespace {
+FwdArgs dgrad_bn_args(int n, int h, int w, int cout, int cin) {
+  FwdArgs a = base_args();
+  a.a_ld = cout;
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cout; a.N = cin; a.M = (long)n * h * w; a.out_ld = cin; a.cout = cin;
+  return a;
+}
+}  // namespace
+
+// Partial-sum rows cnnitmo_conv3x3_dgrad_bn writes (0: the fused path is not
+// available for these sizes / dtype).
+extern "C" long cnnitmo_conv3x3_dgrad_bn_rows(int dtype, int n, int h, int w, int cout, int cin, int c0,
+                                              int c1) {
+  FwdArgs a = dgrad_bn_args(n, h, w, cout, cin);
+  a.bnb_c0 = c0; a.bnb_c1 = c1; a.bnb_out = (void*)1; a.bnb_r_ld = 8;
+  if (dtype != CNNITMO_BF16 || !halo_handles(a)) return 0;
+  return halo_stat_rows(a);
+}
+
+extern "C" int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h, int w, int cout,
+                                        const void* wt_flip, int cin, void* dx, int dx_ld, int dx_off,
+                                        int c0, int c1, const float* coef, const void* r, int r_ld,
+                                        int r_off, void* dz_out, float* part, int parity, void* stream) {
+  FwdArgs a = dgrad_bn_args(n, h, w, cout, cin);
+  a.a = dz; a.b = wt_flip;
+  a.out = dx; a.out_ld = dx ? dx_ld : cin; a.out_off = dx ? dx_off : 0;
+  a.bnb_c0 = c0; a.bnb_c1 = c1; a.bnb_par = parity ? 1 : 0;
+  a.bnb_coef = coef; a.bnb_r = r; a.bnb_r_ld = r_ld; a.bnb_r_off = r_off; a.bnb_out = dz_out;
+  a.stats = part;
+  CNN_REQUIRE(dtype == CNNITMO_BF16 && halo_handles(a), "conv3x3_dgrad_bn: unsupported sizes (bf16 halo only)");
+  CNN_REQUIRE(coef && r && dz_out && part && (dx || (c0 == 0 && c1 == cin)),
+              "conv3x3_dgrad_bn: missing buffers");
+  return launch_halo(a, (hipStream_t)stream, "conv3x3_dgrad_bn");
+}
+
 extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int w, int cin,
                                     const void* k, const float* bias, int cout, void* out,
                                     int out_ld, int out_off, int flags, const float* aff_scale,

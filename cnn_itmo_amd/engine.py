@@ -31,6 +31,7 @@ bucketer (dist.py) all-reduces them in.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import numpy as np
@@ -59,6 +60,7 @@ class Value:
         self.folded = False  # holds r; the true value is r*cs + ch (per channel)
         self.producer = None  # BlockStage writing this value
         self.sum_consumers = 0  # >0: BN-backward sums come from this many consumers (no reduce pass)
+        self.fuse_into = None  # the single conv3x3 consumer whose dgrad applies this BN's backward
         self.bn_contrib = []  # per-step partial-sum tensors [rows][2][c] from the consumers
         self.pool_route = None  # (pooled gradient, argmax idx): a deferred MaxPooling2D backward
         self.cs = None  # coefficient buffers of the owner (persist across steps)
@@ -167,6 +169,7 @@ class BlockStage(Stage):
         if self.vout.folded:
             self.vout.ensure_coef(dev)
         self.fold_active = False
+        self.fused = None  # (dz, part, rows) when the consumer's dgrad applied this stage's BN backward
 
     def prep(self):
         e = self.eng
@@ -272,16 +275,40 @@ class BlockStage(Stage):
             ops.bn_apply(e.dt, r, P, cout, self.scale, self.shift, out, flags, e.drop_seed, self.drop_id)
         self.r = rview
 
+    def bn_coef(self, n):
+        """BN-backward coefficients [3][cout] (and dgamma/dbeta) from the consumer-derived
+        sums alone, for a consumer that applies the BN backward in its dgrad store."""
+        e = self.eng
+        v = self.vout
+        assert v.sum_consumers and len(v.bn_contrib) == v.sum_consumers
+        part = torch.cat(v.bn_contrib)
+        v.bn_contrib = []
+        coef = torch.empty(3 * self.cout, device=e.device, dtype=torch.float32)
+        ops.bn_bwd_finalize(part, part.numel() // (2 * self.cout), self.cout, n * v.h * v.w,
+                            e.p(self.bn.name + "/gamma"), self.smean, self.sinv, e.g(self.bn.name + "/gamma"),
+                            e.g(self.bn.name + "/beta"), coef)
+        return coef
+
     def backward(self, n):
         e = self.eng
         cout = self.cout
         P = n * self.vout.h * self.vout.w
+        par = self.fold_active and self.kind == "t2"  # tconv wgrad fold needs per-tap sums of dz
+        if self.fused is not None:  # dz and its column partials came from the consumer's dgrad
+            dz, part2, rows = self.fused
+            self.fused = None
+        else:
+            dz, part2, rows = self._bn_backward(n, P, par)
+        self._weight_and_input_grads(n, P, par, dz, part2, rows)
+
+    def _bn_backward(self, n, P, par):
+        e = self.eng
+        cout = self.cout
         if not self.vout.ginit:
             raise RuntimeError(f"{self.name}: output gradient not initialised")
         dy = self.vout.gview(n)
         rows = ops.bn_bwd_rows(P, cout)
         dz = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
-        par = self.fold_active and self.kind == "t2"  # tconv wgrad fold needs per-tap sums of dz
         part2 = torch.empty(rows * (4 if par else 1) * cout, device=e.device, dtype=torch.float32)
         flags = (L.DROPOUT if self.drop is not None else 0) | (L.PARITY if par else 0)
         if self.bn is not None:
@@ -314,6 +341,25 @@ class BlockStage(Stage):
         else:
             ops.bn_bwd_apply(e.dt, dy, self.r, cout, None, flags | L.NO_BN, e.drop_seed,
                              self.drop_id, dz, part2)
+        return dz, part2, rows
+
+    def _fused_target(self, n, targets):
+        """The (value, channel offset) among `targets` whose BN backward this stage's dgrad
+        applies (cnnitmo_conv3x3_dgrad_bn), with its partial-sum row count; or None."""
+        e = self.eng
+        if self.kind != "c3" or not e.fuse_bnb or not self.vin.needs_grad:
+            return None
+        for m, ci0 in targets:
+            if m.fuse_into is self and m.sum_consumers == 1:
+                rows = ops.conv3x3_dgrad_bn_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, self.cin, ci0,
+                                                 ci0 + m.c)
+                if rows > 0:
+                    return m, ci0, rows
+        return None
+
+    def _weight_and_input_grads(self, n, P, par, dz, part2, rows):
+        e = self.eng
+        cout = self.cout
         db = e.g(self.conv.name + "/bias")
         dw = e.g(self.conv.name + "/kernel")
         psum = None
@@ -327,7 +373,10 @@ class BlockStage(Stage):
         # it runs on the engine's side stream, overlapping the HBM-bound BN passes and the
         # dgrad on the compute stream.  Tensors it reads are recorded on that stream.
         targets = self._sum_targets() if self.fold_active else []
-        with e.side(dz, psum, getattr(self, "cols", None)):
+        fz = self._fused_target(n, targets)
+        # with a fused producer BN the dgrad needs this weight gradient's sums first
+        ctx = contextlib.nullcontext() if fz else e.side(dz, psum, getattr(self, "cols", None))
+        with ctx:
             raw = torch.empty_like(dw) if targets else None
             if self.kind == "c3in":
                 ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
@@ -356,7 +405,29 @@ class BlockStage(Stage):
                     ops.bn_consumer_sums(2, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, None,
                                          psum, m.producer.smean, m.producer.sinv, pm)
                     m.bn_contrib.append(pm)
-        if self.vin.needs_grad:
+        if fz is not None:
+            m, ci0, frows = fz
+            prod = m.producer
+            coef = prod.bn_coef(n)
+            whole = ci0 == 0 and m.c == self.cin
+            dx = None
+            if not whole:
+                if self.vin.ginit:
+                    raise NotImplementedError(f"{self.name}: input gradient would need accumulation")
+                self.vin.ensure_grad(n, e.tdtype, e.device)
+                dx = self.vin.gview(n)
+            ppar = prod.fold_active and prod.kind == "t2"
+            dzp = torch.empty(P * m.c, dtype=e.tdtype, device=e.device)
+            pp = torch.empty(frows * (4 if ppar else 1) * m.c, device=e.device, dtype=torch.float32)
+            ops.conv3x3_dgrad_bn(e.dt, dz, n, self.vout.h, self.vout.w, cout, self.w_bwd, self.cin, dx, ci0,
+                                 ci0 + m.c, coef, prod.r, dzp, pp, ppar)
+            prod.fused = (dzp, pp, frows)
+            if not whole:
+                if self.vin.place:
+                    self.vin.ginit = True
+                else:
+                    self.vin.mark_grad()
+        elif self.vin.needs_grad:
             if self.vin.ginit:
                 raise NotImplementedError(f"{self.name}: input gradient would need accumulation")
             self.vin.ensure_grad(n, e.tdtype, e.device)
@@ -583,6 +654,8 @@ def _plan_bn_sums(stages):
             (isinstance(r, BlockStage) and r.kind in ("c3", "t2")) or isinstance(r, (PoolStage, HeadStage))
             for r in rs)
         v.sum_consumers = len(rs) if ok else 0
+        v.fuse_into = rs[0] if (ok and len(rs) == 1 and isinstance(rs[0], BlockStage) and rs[0].kind == "c3") \
+            else None
 
 
 def layout_params(stages):
@@ -634,6 +707,8 @@ class Engine:
         self.grad_hook = None  # callable(lo, hi) after each stage's gradients are written
         self._side = None  # side stream for weight gradients (CNNITMO_SIDE_STREAM=0: off)
         self._side_on = os.environ.get("CNNITMO_SIDE_STREAM", "1") != "0"
+        # consumer dgrads apply their producer's BN backward (CNNITMO_FUSE_BNB=0: separate pass)
+        self.fuse_bnb = os.environ.get("CNNITMO_FUSE_BNB", "1") != "0"
         self._side_keep = []
 
     # ---- parameter access ---------------------------------------------------
@@ -684,7 +759,6 @@ class Engine:
         """Context running its work on the side stream after everything queued so far
         on the compute stream; `tensors` (allocated on the compute stream) are kept
         alive for it.  Without a side stream: a no-op context."""
-        import contextlib
         if not self._side_on:
             return contextlib.nullcontext()
         if self._side is None:

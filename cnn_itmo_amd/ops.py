@@ -90,6 +90,18 @@ def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx: View):
          stream_ptr())
 
 
+def conv3x3_dgrad_bn_rows(dt, n, h, w, cout, cin, c0, c1):
+    return query("cnnitmo_conv3x3_dgrad_bn_rows", dt, n, h, w, cout, cin, c0, c1)
+
+
+def conv3x3_dgrad_bn(dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1, coef, r, dz_out, part, parity):
+    """conv3x3_dgrad with the producer's BN backward fused (see cnn_itmo.h); dx: View or None."""
+    rp, rld, roff = _rview(r, c1 - c0)
+    call("cnnitmo_conv3x3_dgrad_bn", dt, ptr(dz), n, h, w, cout, ptr(wflip), cin,
+         dx.ptr if dx is not None else None, dx.ld if dx is not None else cin, dx.off if dx is not None else 0,
+         c0, c1, ptr(coef), rp, rld, roff, ptr(dz_out), ptr(part), 1 if parity else 0, stream_ptr())
+
+
 def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0, fold=None, raw=None):
     """fold = (scale, shift, db, border_sums) for a folded input BN, else None;
     raw (optional, dw-shaped fp32): the uncorrected dz (x) r sum."""

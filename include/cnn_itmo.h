@@ -97,6 +97,22 @@ long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int cin, int cou
 int cnnitmo_conv3x3_dgrad(int dtype, const void* dz, int n, int h, int w, int cout,
                           const void* wt_flip, int cin, void* dx, int dx_ld, int dx_off,
                           void* stream);
+/* conv3x3_dgrad with the PRODUCER's BN backward fused into its store (bf16):
+ * input-gradient columns [c0, c1) are the gradient g of a folded BN output
+ * whose backward coefficients coef [3][c1-c0] (cnnitmo_bn_bwd_finalize) are
+ * already known (consumer-derived sums); they are written as the producer's
+ * dz = [r>0]*(a*g - b*r + e) to dz_out [n*h*w][c1-c0] (r: the producer's saved
+ * view, element (p, j) at r[p*r_ld + r_off + j]) together with column-sum
+ * partials part [rows][parity ? 4 : 1][c1-c0] (rows =
+ * cnnitmo_conv3x3_dgrad_bn_rows; parity splits by (h&1, w&1) like
+ * CNNITMO_PARITY).  Columns outside [c0, c1) go to dx as in conv3x3_dgrad (dx
+ * may be NULL when [c0, c1) = [0, cin)).  Replaces conv3x3_dgrad +
+ * cnnitmo_bn_bwd_apply.  rows = 0: not available for these sizes. */
+long cnnitmo_conv3x3_dgrad_bn_rows(int dtype, int n, int h, int w, int cout, int cin, int c0, int c1);
+int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h, int w, int cout,
+                             const void* wt_flip, int cin, void* dx, int dx_ld, int dx_off, int c0,
+                             int c1, const float* coef, const void* r, int r_ld, int r_off,
+                             void* dz_out, float* part, int parity, void* stream);
 
 /* Weight-gradient of conv3x3 (TF Conv2DBackpropFilter).  x view [n,h,w,cin];
  * dz [n,h,w,cout] contiguous; dw: [cout][3][3][cin] fp32, OVERWRITTEN.
