@@ -39,9 +39,23 @@ __device__ __attribute__((aligned(256))) uint4 h_sink[64];
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
-__device__ __forceinline__ void glds16(const void* gsrc, const char* lds) {
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// raw buffer descriptor over [base, base + 2 GB): a load at voffset >= OOB_OFF is
+// dropped by the range check and lands zeros (halo padding, pad rows)
+constexpr unsigned OOB_OFF = 0x80000000u;
+__device__ __forceinline__ i32x4 buf_rsrc(uintptr_t base) {
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
+  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xFFFF;
+  r.z = 0x7FFFFFF0;
+  r.w = 0x00020000;
+  return r;
+}
+// one 16-byte piece per lane -> the wave's 1 KiB LDS image at `lds` (LDS-DMA)
+__device__ __forceinline__ void blds16(unsigned voff, i32x4 rs, const char* lds) {
   const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr(lds));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(a) : "m0");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "s"(a) : "memory");
 }
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -161,49 +175,42 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
   // per-lane load geometry, fixed for the whole launch: one glds instruction =
   // 16 LDS rows x 4 pieces of 16 B; lane -> (row, piece), source piece swizzled
   const int lrow = lane >> 2, lpc = lane & 3;
+  constexpr int lo = MODE == 0 ? 1 : 0;  // halo reach above / left of the tile
   int ppy[NPI], ppx[NPI];
-  long poff[NPI];  // element offset of the lane's source piece from the tile origin
+  unsigned poff[NPI];  // byte offset of the lane's source piece from the patch origin (tile origin - lo rows/cols)
 #pragma unroll
   for (int i = 0; i < NPI; ++i) {
     const int row = (wave * NPI + i) * 16 + lrow;
     const int piece = lpc ^ (((row >> 2) & 1) << 1);
     const int py = row / PW, px = row - (row / PW) * PW;
-    const int dy = MODE == 0 ? py - 1 : py, dx = MODE == 0 ? px - 1 : px;  // source offset from the tile origin
-    ppy[i] = row < C::PROWS ? dy : -(1 << 29);  // padded rows: never in bounds, never loaded
-    ppx[i] = dx;
-    poff[i] = ((long)dy * p.ws + dx) * p.a_ld + piece * 8;
+    ppy[i] = row < C::PROWS ? py - lo : -(1 << 29);  // padded rows: never in bounds, never loaded
+    ppx[i] = px - lo;
+    poff[i] = (unsigned)((((long)py * p.ws + px) * p.a_ld + piece * 8) * 2);
   }
-  int boff[NBI];
+  unsigned boff[NBI];
 #pragma unroll
   for (int i = 0; i < NBI; ++i) {
     const int row = (wave * NBI + i) * 16 + lrow;  // = tap * BN + n
     const int piece = lpc ^ (((row >> 2) & 1) << 1);
     const int tap = row / BN, n = row - (row / BN) * BN;
-    boff[i] = row < C::B_ROWS ? n * K + tap * p.cin + piece * 8 : -1;
+    boff[i] = row < C::B_ROWS ? (unsigned)((n * K + tap * p.cin + piece * 8) * 2) : OOB_OFF;
   }
 
   auto issue = [&](int buf) {
     const Pos& s = ip;
     char* Ps = smem + buf * STAGE;
     char* Bs = Ps + C::PATCH;
-    const bf16* tb = X + ((size_t)((long)s.img * p.hs + s.y0) * p.ws + s.x0) * p.a_ld + p.a_off + s.ch * 32;
-    constexpr int lo = MODE == 0 ? 1 : 0;  // halo reach above / left of the tile
-    const bool interior = s.y0 >= lo && s.y0 + TH + lo <= p.hs && s.x0 >= lo && s.x0 + TW + lo <= p.ws;
+    const long po = ((long)s.img * p.hs + s.y0 - lo) * p.ws + s.x0 - lo;  // patch origin pixel (may be < 0)
+    const i32x4 prs = buf_rsrc((uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + s.ch * 32) * 2));
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
-      const void* src = h_zero_page;
-      if (interior) {
-        if (ppy[i] > -(1 << 28)) src = tb + poff[i];
-      } else {
-        const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
-        if ((unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws) src = tb + poff[i];
-      }
-      glds16(src, Ps + (wave * NPI + i) * 1024);
+      const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
+      const bool ok = (unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws;
+      blds16(ok ? poff[i] : OOB_OFF, prs, Ps + (wave * NPI + i) * 1024);
     }
-    const bf16* bb = Wt + (size_t)s.nb * BN * K + s.ch * 32;
+    const i32x4 brs = buf_rsrc((uintptr_t)(Wt + (size_t)s.nb * BN * K + s.ch * 32));
 #pragma unroll
-    for (int i = 0; i < NBI; ++i)
-      glds16(boff[i] >= 0 ? (const void*)(bb + boff[i]) : (const void*)h_zero_page, Bs + (wave * NBI + i) * 1024);
+    for (int i = 0; i < NBI; ++i) blds16(boff[i], brs, Bs + (wave * NBI + i) * 1024);
   };
 
   f32x4 acc[FM][FN];
