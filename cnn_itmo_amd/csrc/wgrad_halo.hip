@@ -26,16 +26,27 @@
 
 #pragma clang diagnostic ignored "-Winline-asm"
 
-static __device__ __attribute__((aligned(256))) unsigned char wh_zero_page[256] = {0};
-
 namespace {
 
 __device__ __forceinline__ unsigned lds_addr3(const void* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
-__device__ __forceinline__ void glds(const void* gsrc, const char* lds) {
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// raw buffer descriptor over [base, base + 2 GB): loads at voffset >= OOB_OFF are
+// dropped by the range check and land zeros (image edges, overhanging strips)
+constexpr unsigned OOB_OFF = 0x80000000u;
+__device__ __forceinline__ i32x4 buf_rsrc(uintptr_t base) {
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
+  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xFFFF;
+  r.z = 0x7FFFFFF0;
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void blds(unsigned voff, i32x4 rs, const char* lds) {
   const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr3(lds));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(a) : "m0");
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "s"(a) : "memory");
 }
 template <int N> __device__ __forceinline__ void waitvm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 __device__ __forceinline__ void waitvm_dyn(int n) {
@@ -118,8 +129,8 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 
   // ---- per-lane DMA geometry (fixed for the launch) --------------------------
   // x row image: XROWS pixel rows (columns x0-1 .. x0+TW) of BN channels
-  int xoff[LX];  // element offset from pixel (row g, column x0)
-  bool xact[LX], xval[LX];  // lane issues this DMA / its pixel is inside the image
+  unsigned xoff[LX];  // byte offset from pixel (row g, column x0 - 1), OOB_OFF outside the image
+  bool xact[LX];      // this wave issues DMA q
 #pragma unroll
   for (int q = 0; q < LX; ++q) {
     const int ins = wave + q * NW;
@@ -128,11 +139,10 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     const int row = off / (BN * 2), pos = off - row * (BN * 2);
     const int col = (((pos >> 5) ^ trswz<BN>(row)) << 4) + ((pos >> 4) & 1) * 8;
     const int xx = x0 - 1 + row;
-    xval[q] = row < C::XROWS && xx >= 0 && xx < p.W;
-    xoff[q] = (int)((row - 1) * p.x_ld) + col;
+    xoff[q] = row < C::XROWS && xx >= 0 && xx < p.W ? (unsigned)((row * p.x_ld + col) * 2) : OOB_OFF;
   }
-  int doff[LD];
-  bool dact[LD], dval[LD];  // (the last strip may overhang the image: zero columns)
+  unsigned doff[LD];
+  bool dact[LD];  // (the last strip may overhang the image: zero columns)
 #pragma unroll
   for (int q = 0; q < LD; ++q) {
     const int ins = wave + q * NW;
@@ -140,8 +150,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     const int off = ins * 1024 + lane * 16;
     const int row = off / (BM * 2), pos = off - row * (BM * 2);
     const int col = (((pos >> 5) ^ trswz<BM>(row)) << 4) + ((pos >> 4) & 1) * 8;
-    doff[q] = row * p.cout + col;
-    dval[q] = x0 + row < p.W;
+    doff[q] = x0 + row < p.W ? (unsigned)((row * p.cout + col) * 2) : OOB_OFF;
   }
   int nx = 0, nd = 0;  // DMA instructions this wave issues per x / dz row
 #pragma unroll
@@ -152,18 +161,18 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
   auto issue_x = [&](long g, int slot) {
     char* S = xbase + slot * XB * 1024;
     const bool ok = g >= 0 && g < total_rows;
-    const bf16* base = p.x + ((size_t)g * p.W + x0) * p.x_ld + p.x_off + n0;
+    const long e0 = ((long)g * p.W + x0 - 1) * p.x_ld + p.x_off + n0;  // may be < 0 (first pixel)
+    const i32x4 rs = buf_rsrc((uintptr_t)p.x + (uintptr_t)(e0 * 2));
 #pragma unroll
     for (int q = 0; q < LX; ++q)
-      if (xact[q]) glds(ok && xval[q] ? (const void*)(base + xoff[q]) : (const void*)wh_zero_page,
-                        S + (wave + q * NW) * 1024);
+      if (xact[q]) blds(ok ? xoff[q] : OOB_OFF, rs, S + (wave + q * NW) * 1024);
   };
   auto issue_d = [&](long g, int slot) {
     char* S = dbase + slot * DB * 1024;
-    const bf16* base = p.dz + ((size_t)g * p.W + x0) * p.cout + m0;
+    const i32x4 rs = buf_rsrc((uintptr_t)(p.dz + ((size_t)g * p.W + x0) * p.cout + m0));
 #pragma unroll
     for (int q = 0; q < LD; ++q)
-      if (dact[q]) glds(dval[q] ? (const void*)(base + doff[q]) : (const void*)wh_zero_page, S + (wave + q * NW) * 1024);
+      if (dact[q]) blds(doff[q], rs, S + (wave + q * NW) * 1024);
   };
 
   f32x4 acc[3][FM][FN];  // taps (wr, s), s = 0..2
