@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libcnnitmo.so")
+LIB_PATH = os.environ.get("CNNITMO_LIB") or os.path.join(HERE, "lib", "libcnnitmo.so")  # override: experiments
 
 F32 = 0
 BF16 = 1

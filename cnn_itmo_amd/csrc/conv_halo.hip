@@ -27,6 +27,14 @@
 
 #include "igemm_common.h"
 
+// timing-only experiment builds (tools/halo_exp.sh), results are garbage:
+// 1 = no DMA wait, 2 = no MFMA, 3 = no epilogue, 4 = no DMA issue/wait,
+// 5 = epilogue without its global stores, 6 = epilogue without the C-tile LDS writes,
+// 7 = epilogue without C-tile LDS writes and barriers
+#ifndef HALO_EXP
+#define HALO_EXP 0
+#endif
+
 namespace {
 
 __device__ __attribute__((aligned(256))) unsigned char h_zero_page[256] = {0};
@@ -196,21 +204,31 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
     boff[i] = row < C::B_ROWS ? (unsigned)((n * K + tap * p.cin + piece * 8) * 2) : OOB_OFF;
   }
 
-  auto issue = [&](int buf) {
+  // The loads of an item are prepared once (descriptors, per-piece offsets) and
+  // issued piece by piece: the main loop spreads them between the taps of the
+  // previous item's MFMAs, so LDS-DMA issue overlaps matrix work instead of
+  // stalling every wave at the top of the chunk.
+  constexpr int L = NPI + NBI;  // LDS-DMA instructions per wave per item
+  uintptr_t pbase = 0, bbase = 0;  // descriptor bases (built into SGPRs at each use)
+  char* iPs = smem;
+  unsigned pvo[NPI];
+  auto issue_prep = [&](int buf) {
     const Pos& s = ip;
-    char* Ps = smem + buf * STAGE;
-    char* Bs = Ps + C::PATCH;
+    iPs = smem + buf * STAGE;
     const long po = ((long)s.img * p.hs + s.y0 - lo) * p.ws + s.x0 - lo;  // patch origin pixel (may be < 0)
-    const i32x4 prs = buf_rsrc((uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + s.ch * 32) * 2));
+    pbase = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + s.ch * 32) * 2);
+    bbase = (uintptr_t)(Wt + (size_t)s.nb * BN * K + s.ch * 32);
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
       const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
       const bool ok = (unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws;
-      blds16(ok ? poff[i] : OOB_OFF, prs, Ps + (wave * NPI + i) * 1024);
+      pvo[i] = ok ? poff[i] : OOB_OFF;
     }
-    const i32x4 brs = buf_rsrc((uintptr_t)(Wt + (size_t)s.nb * BN * K + s.ch * 32));
-#pragma unroll
-    for (int i = 0; i < NBI; ++i) blds16(boff[i], brs, Bs + (wave * NBI + i) * 1024);
+  };
+  auto issue_piece = [&](int k) {  // k: compile-time after unrolling
+    if constexpr (HALO_EXP == 4) return;
+    if (k < NPI) blds16(pvo[k], buf_rsrc(pbase), iPs + (wave * NPI + k) * 1024);
+    else blds16(boff[k - NPI], buf_rsrc(bbase), iPs + C::PATCH + (wave * NBI + k - NPI) * 1024);
   };
 
   f32x4 acc[FM][FN];
@@ -231,25 +249,43 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
 #pragma unroll
   for (int k = 0; k < 8; ++k) apre[k] = rbase * 64 + ((fpc ^ ((((rbase + k) >> 2) & 1) << 1)) << 4);
   const int bpre = frow * 64 + ((fpc ^ (((frow >> 2) & 1) << 1)) << 4);
-  auto compute = [&](int buf) {
+  // Fragments are double-buffered across taps: tap t+1's ds_reads are issued
+  // before tap t's MFMAs (pinned by sched barriers), so a whole tap of MFMAs
+  // covers their latency instead of the just-in-time reads the scheduler emits.
+  auto compute = [&](int buf, bool pf) {
     const char* Ps = smem + buf * STAGE;
     const char* Bs = Ps + C::PATCH;
-#pragma unroll
-    for (int tap = 0; tap < KT; ++tap) {
+    uint4 af[2][FM], bfr[2][FN];
+    auto load = [&](int tap, int sl) {
       const int r = MODE == 0 ? tap / 3 : 0, s = MODE == 0 ? tap - 3 * (tap / 3) : 0;
-      uint4 af[FM], bfr[FN];
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         const int c = (f / FMR + r) * PW + (f % FMR) * 16 + s;  // tile row f/FMR of this wave
-        af[f] = *reinterpret_cast<const uint4*>(Ps + apre[c & 7] + c * 64);
+        af[sl][f] = *reinterpret_cast<const uint4*>(Ps + apre[c & 7] + c * 64);
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        bfr[j] = *reinterpret_cast<const uint4*>(Bs + bpre + (tap * BN + j * 16) * 64);
+        bfr[sl][j] = *reinterpret_cast<const uint4*>(Bs + bpre + (tap * BN + j * 16) * 64);
+    };
+    load(0, 0);
+#pragma unroll
+    for (int tap = 0; tap < KT; ++tap) {
+      const int cur = tap & 1;
+      if (tap + 1 < KT) load(tap + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], af[i], bfr[j]);
+        for (int j = 0; j < FN; ++j)
+          if constexpr (HALO_EXP == 2) acc[i][j][0] += __builtin_bit_cast(float, af[cur][i].x ^ bfr[cur][j].y);
+          else Mma<bf16>::run(acc[i][j], af[cur][i], bfr[cur][j]);
+      // the next item's LDS-DMA pieces due after this tap
+      if (pf) {
+#pragma unroll
+        for (int k = 0; k < L; ++k)
+          if ((k * KT) / L == tap) issue_piece(k);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -285,7 +321,8 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
           const float vs = (oh < p.ho && x0 + col < p.wo) ? v : 0.f;  // partial tiles: valid pixels only
           s1[j] += vs;
           s2[j] += vs * vs;
-          Cs[(rr * TW + col) * C::CLD + j * 16 + (lane & 15)] = from_f32<bf16>(v);
+          if constexpr (HALO_EXP != 6 && HALO_EXP != 7) Cs[(rr * TW + col) * C::CLD + j * 16 + (lane & 15)] = from_f32<bf16>(v);
+          else if (p.N < 0) Cs[0] = from_f32<bf16>(v);
         }
     }
     if (stats) {
@@ -304,7 +341,7 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
         }
       }
     }
-    __syncthreads();
+    if constexpr (HALO_EXP != 7) __syncthreads();
     if (stats && tid < C::SG * BN) {
       // one partial-sum row per 256 pixels: rows = M / 256 (= cnnitmo_fwd_stat_rows)
       const int g = tid / BN, col = tid - g * BN;
@@ -336,7 +373,11 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
       uint4* dst = (oh < p.ho && x0 + col < p.wo)
                        ? reinterpret_cast<uint4*>(O + (size_t)(mrow + PSTEP * col) * p.out_ld + p.out_off + co)
                        : h_sink + lane;
-      *dst = v;
+      if constexpr (HALO_EXP == 5) {
+        if (p.N < 0) *dst = v;
+      } else {
+        *dst = v;
+      }
     }
     zero_acc();
   };
@@ -486,7 +527,6 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
   // exactly the older ones (the younger loads and stores stay in flight).  The
   // count is a lower bound for waves whose stats stores were exec-masked off,
   // which only makes their wait stricter.
-  constexpr int L = NPI + NBI;
   // output store instructions per wave
   constexpr int NST = EPI ? RPW * TW * CPRP / 64 : (RPW * TW * CPR + 63) / 64;
   static_assert(RPW * TW * CPR % 64 == 0, "every lane issues the same number of stores");
@@ -500,7 +540,9 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
   for (int k = 0; k < ST - 1; ++k) {
     mq[k] = issued;
     if (k < T) {
-      issue(k);
+      issue_prep(k);
+#pragma unroll
+      for (int q = 0; q < L; ++q) issue_piece(q);
       step(ip);
       issued += L;
       mq[k] = issued;
@@ -509,22 +551,35 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
   mq[ST - 1] = issued;
   int buf = 0;  // stage of item t
   for (long t = 0; t < T; ++t) {
-    wait_vm_dyn(issued - mq[0]);
+    if constexpr (HALO_EXP != 1 && HALO_EXP != 4) wait_vm_dyn(issued - mq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (t + ST - 1 < T) {
-      issue(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
+    const bool pf = t + ST - 1 < T;
+    if (pf) issue_prep(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
+    compute(buf, pf);  // issues those loads between its taps
+    if (pf) {
       step(ip);
       issued += L;
       mq[ST - 1] = issued;
     }
-    compute(buf);
     if (ep.ch == nch - 1) {
-      __syncthreads();  // every wave is done reading this stage: reuse it for the C tile
-      if constexpr (EPI == 1) epilogue_bnb(ep, buf);
-      else epilogue(ep, buf);
-      issued += S;
+      if constexpr (HALO_EXP != 7) __syncthreads();  // every wave is done reading this stage: reuse it for the C tile
+      if constexpr (HALO_EXP == 3) {
+        if (p.N < 0) {  // never: keeps the MFMA results alive
+          float t = 0.f;
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+          ((float*)p.out)[tid] = t;
+        }
+        zero_acc();
+      } else {
+        if constexpr (EPI == 1) epilogue_bnb(ep, buf);
+        else epilogue(ep, buf);
+        issued += S;
+      }
     }
     step(ep);
 #pragma unroll
