@@ -37,6 +37,8 @@ SIGNATURES = {
     "cnnitmo_last_error": (C.c_char_p, []),
     "cnnitmo_conv3x3_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp]),
     "cnnitmo_fwd_stat_rows": (i32, [i32, i64, i32]),
+    "cnnitmo_tconv2x2_dgrad_bn_rows": (i64, [i32, i32, i32, i32, i32, i32]),
+    "cnnitmo_tconv2x2_dgrad_bn": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, vp, vp, vp]),
     "cnnitmo_conv3x3_dgrad_bn_rows": (i64, [i32, i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_conv3x3_dgrad_bn": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32,
                                        i32, vp, vp, i32, vp]),

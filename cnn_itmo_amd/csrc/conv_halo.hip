@@ -655,7 +655,11 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
   if (a.ntaps == 1 && a.scale == 1 && a.scatter && a.hs == a.ho && a.ws == a.wo && a.cout % 32 == 0 &&
       a.N == 4 * a.cout) {
     pl.mode = 1;
-    pl.bn = 128;  // a block may span taps: pieces are scattered one by one
+    static const int m1bn = [] {
+      const char* e = getenv("CNNITMO_HALO_M1BN");
+      return e ? atoi(e) : 128;
+    }();
+    pl.bn = m1bn == 64 ? 64 : 128;  // a block may span taps: pieces are scattered one by one
     pl.th = 8;
     pl.tw = 32;
     return true;

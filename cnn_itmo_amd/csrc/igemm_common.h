@@ -84,6 +84,16 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what);
 const char* halo_name(const FwdArgs& a);
 long halo_stat_rows(const FwdArgs& a);
 
+// tconv_stream.hip: Conv2DTranspose fwd (mode 0) / input-gradient (mode 1) as a
+// streamed GEMM with the weight block resident in LDS (bf16)
+bool tconv_stream_handles(int mode, int h, int w, int cin, int cout, bool epi);
+long tconv_stream_rows(int n, int h, int w);
+const char* tconv_stream_name(int mode, int h, int w, int cin, int cout, bool epi);
+int launch_tconv_stream(int mode, const void* a, long a_ld, int a_off, const void* b, int n, int h, int w,
+                        int cin, int cout, void* out, long out_ld, int out_off, const float* bias, int flags,
+                        const float* aff_scale, const float* aff_shift, float* stats, const float* coef,
+                        const void* r, long r_ld, int r_off, hipStream_t s, const char* what);
+
 // v2 (direct-to-LDS, multi-tap) bf16 weight gradients, igemm_wgrad2.hip
 struct Wgrad2Args {
   const bf16* a;  // A operand source (gradient): channels m

@@ -337,6 +337,7 @@ extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int ci
 }
 
 extern "C" long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int cin, int cout) {
+  if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false)) return tconv_stream_rows(n, h, w);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
   a.cin = cin; a.N = 4 * cout; a.a_ld = cin; a.out_ld = cout; a.M = (long)n * h * w;
@@ -397,6 +398,8 @@ extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int 
 
 extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int w, int cin, int cout,
                                                     int dgrad) {
+  if (dtype == CNNITMO_BF16 && tconv_stream_handles(dgrad ? 1 : 0, h, w, cin, cout, false))
+    return tconv_stream_name(dgrad ? 1 : 0, h, w, cin, cout, false);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
   a.cin = dgrad ? cout : cin;
@@ -494,6 +497,9 @@ extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int 
   a.scatter = 1; a.cout = cout; a.flags = flags;
   a.aff_scale = aff_scale; a.aff_shift = aff_shift; a.stats = stat_part;
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || stat_part, "tconv2x2_fwd: STATS without buffer");
+  if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false))
+    return launch_tconv_stream(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
+                               aff_shift, stat_part, nullptr, nullptr, 0, 0, (hipStream_t)stream, "tconv2x2_fwd");
   return dispatch(dtype, a, stream, "tconv2x2_fwd");
 }
 
@@ -510,5 +516,23 @@ extern "C" int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h,
   }
   a.cin = cout; a.b = kT; a.N = cin; a.M = (long)n * h * w;
   a.out = dx; a.out_ld = cin; a.out_off = 0; a.cout = cin;
+  if (dtype == CNNITMO_BF16 && tconv_stream_handles(1, h, w, cin, cout, false))
+    return launch_tconv_stream(1, dout, cout, 0, kT, n, h, w, cin, cout, dx, cin, 0, nullptr, 0, nullptr, nullptr,
+                               nullptr, nullptr, nullptr, 0, 0, (hipStream_t)stream, "tconv2x2_dgrad");
   return dispatch(dtype, a, stream, "tconv2x2_dgrad");
+}
+
+extern "C" long cnnitmo_tconv2x2_dgrad_bn_rows(int dtype, int n, int h, int w, int cout, int cin) {
+  if (dtype != CNNITMO_BF16 || !tconv_stream_handles(1, h, w, cin, cout, true)) return 0;
+  return tconv_stream_rows(n, h, w);
+}
+
+extern "C" int cnnitmo_tconv2x2_dgrad_bn(int dtype, const void* dout, int n, int h, int w, int cout,
+                                         const void* kT, int cin, const float* coef, const void* r, int r_ld,
+                                         int r_off, void* dz_out, float* part, void* stream) {
+  CNN_REQUIRE(dtype == CNNITMO_BF16 && tconv_stream_handles(1, h, w, cin, cout, true),
+              "tconv2x2_dgrad_bn: unsupported sizes (bf16 stream kernel only)");
+  CNN_REQUIRE(coef && r && dz_out && part, "tconv2x2_dgrad_bn: missing buffers");
+  return launch_tconv_stream(1, dout, cout, 0, kT, n, h, w, cin, cout, dz_out, cin, 0, nullptr, 0, nullptr,
+                             nullptr, part, coef, r, r_ld, r_off, (hipStream_t)stream, "tconv2x2_dgrad_bn");
 }

@@ -1,0 +1,526 @@
+// Conv2DTranspose(2, strides=2) forward and input-gradient (model.py
+// ConvBNTranspose: up6..up9) as streamed GEMMs with the weight block RESIDENT in
+// LDS.  Both are HBM-bound (K = cin or 4*cout <= 2048, one pass over the
+// activations), so the kernel is built to stream:
+//   * a persistent workgroup per CU owns ONE column block (nb) of the GEMM for
+//     its whole life: its weight block (K x BN bf16 <= 64 KB) is DMA'd once,
+//   * the activations stream through an LDS-DMA ring (64-pixel tiles x 128-deep
+//     K chunks, 16 KB per stage), each byte read from HBM once per column block,
+//   * the MFMA runs with the operands swapped (C^T = W^T A^T), so a lane ends up
+//     with 4 consecutive output channels of one pixel and stores them straight
+//     from registers (8-byte buffer stores, out-of-range pixels dropped by the
+//     range check): no LDS staging, no barrier in the epilogue.
+// MODE 0 (forward): A = x [P][cin] (a row per input pixel), B = k [4*cout][cin];
+//   GEMM column n = tap*cout + co is scattered to output pixel (2y+a, 2x+b).
+//   Epilogue: bias (per column), ReLU, inference affine, BN partial sums.
+// MODE 1 (input gradient): A row of output pixel (y, x) = the four dout pixels
+//   (2y+a, 2x+b) x cout (K = tap*cout + co), B = kT [cin][4*cout].
+//   EPI: the producer's BN backward fused into the store (as the conv3x3 dgrad's
+//   halo EPI 1): dz = [r>0]*(a*g - b*r + e) of the bf16-rounded g, r DMA'd with
+//   the tile's last chunk, plus column sums of dz.
+#include <algorithm>
+#include <cstdio>
+
+#include "igemm_common.h"
+
+namespace {
+
+#pragma clang diagnostic ignored "-Winline-asm"
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4_ __attribute__((ext_vector_type(4)));
+constexpr unsigned OOB = 0x80000000u;  // voffset beyond num_records: load zeros / drop store
+
+__device__ __forceinline__ unsigned lds_u32(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ i32x4 rsrc_of(uintptr_t base) {
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
+  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xFFFF;
+  r.z = 0x7FFFFFF0;
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void dma16(unsigned voff, i32x4 rs, const char* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane(lds_u32(lds));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "s"(a) : "memory");
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t srsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFF0, 0x00020000);
+}
+template <int N> __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void vmwait_dyn(int n) {
+  switch (n) {
+#define W1(k) case k: vmwait<k>(); break;
+    W1(0) W1(1) W1(2) W1(3) W1(4) W1(5) W1(6) W1(7) W1(8) W1(9) W1(10) W1(11) W1(12) W1(13) W1(14) W1(15)
+    W1(16) W1(17) W1(18) W1(19) W1(20) W1(21) W1(22) W1(23) W1(24) W1(25) W1(26) W1(27) W1(28) W1(29)
+    W1(30) W1(31)
+#undef W1
+    default: vmwait<0>(); break;
+  }
+}
+// sum over the 16 lanes of each DPP row (lanes = pixels of a fragment): xor 1, xor 2
+// (quad_perm), then half-row and row mirrors; 4 VALU ops, no LDS crossbar traffic
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+// 64-byte LDS rows, 16-byte piece c of row q at c ^ (((q >> 2) & 1) << 1): every
+// ds_read_b128 fragment window (16 consecutive rows) is conflict-free
+// (tools/check_swizzle.py, the halo kernel's image).
+__device__ __forceinline__ int rsw(int row, int piece) { return (row << 6) + ((piece ^ (((row >> 2) & 1) << 1)) << 4); }
+
+struct TSArgs {
+  const bf16* a;   // MODE 0: x view base (+a_off), row stride a_ld; MODE 1: dout [n][2h][2w][cout]
+  long a_ld;
+  int a_off;
+  const bf16* b;   // [N][K]
+  int nimg, h, w;  // the small grid (tconv input / input-gradient)
+  int cout;        // layer output channels
+  int K, N, nblocks, tiles_x;
+  long ntiles;     // nimg * h * tiles_x
+  bf16* out;       // MODE 0: [n][2h][2w] x out_ld (+out_off); MODE 1: [P] x out_ld (+out_off)
+  long out_ld;
+  int out_off;
+  const float* bias;  // MODE 0, per GEMM column (CNNITMO_BIAS_PER_COL) or per co
+  int flags;
+  const float* aff_scale;
+  const float* aff_shift;
+  float* stats;  // MODE 0: [ntiles*2][2][N]; MODE 1 EPI: [ntiles*2][N] sums of dz
+  const float* coef;  // MODE 1 EPI: [3][N]
+  const bf16* r;
+  long r_ld;
+  int r_off;
+};
+
+template <int MODE, int BN, int ST, bool EPI>
+struct TSCfg {
+  static constexpr int NT = 512, BM = 64, KC = 128;  // 8 waves: 2 (pixels) x 4 (columns)
+  static constexpr int FM = 2, FN = BN / 64;          // wave tile 32 px x BN/4 columns
+  static constexpr int STAGE = BM * KC * 2;           // 16 KB
+  static constexpr int RSLOT = EPI ? BM * BN * 2 : 0;
+  static constexpr int PAR = 3 * BN * 4;
+  static constexpr int BRES = 64 * 1024;
+  static constexpr int SMEM = BRES + PAR + ST * STAGE + 2 * RSLOT;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+template <int MODE, int BN, int ST, bool EPI>
+__global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
+  using C = TSCfg<MODE, BN, ST, EPI>;
+  constexpr int FM = C::FM, FN = C::FN, STAGE = C::STAGE;
+  constexpr int PPR = BN / 8;  // 16-byte pieces per R row
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  char* const Bres = smem;
+  float* const par = reinterpret_cast<float*>(smem + C::BRES);
+  char* const ring = smem + C::BRES + C::PAR;
+  char* const rr = ring + ST * STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (b % 8); the
+  // column blocks of one tile range live on the SAME XCD, so the re-reads of an
+  // A tile by the other column blocks hit that XCD's L2
+  const int G = gridDim.x / p.nblocks;
+  const int xcd = blockIdx.x & 7, wi = blockIdx.x >> 3, per_xcd = gridDim.x >> 3;
+  const int lid = xcd * per_xcd + wi;  // consecutive lids share an XCD
+  const int nb = lid % p.nblocks, g = lid / p.nblocks;
+  const long per = (p.ntiles + G - 1) / G;
+  const long t0 = (long)g * per, t1 = t0 + per < p.ntiles ? t0 + per : p.ntiles;
+  if (t0 >= t1) return;
+  const int K = p.K, nch = K / C::KC, n0 = nb * BN;
+
+  // ---- resident weight block + per-column parameters (once) -------------------
+  {
+    const int rows = K / 32 * BN;  // 64-byte rows: row = kstep * BN + n
+    const i32x4 rs = rsrc_of((uintptr_t)(p.b + (size_t)n0 * K));
+    for (int q = wave; q < rows / 16; q += 8) {
+      const int row = q * 16 + (lane >> 2), piece = (lane & 3) ^ (((row >> 2) & 1) << 1);
+      const int ks = row / BN, n = row - ks * BN;
+      dma16((unsigned)((n * K + ks * 32 + piece * 8) * 2), rs, Bres + q * 1024);
+    }
+    for (int c = tid; c < BN; c += C::NT) {
+      const int n = n0 + c;
+      if constexpr (MODE == 0) {
+        const int co = n % p.cout;
+        par[c] = p.bias ? p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : co] : 0.f;
+        par[BN + c] = (p.flags & CNNITMO_AFFINE) ? p.aff_scale[co] : 1.f;
+        par[2 * BN + c] = (p.flags & CNNITMO_AFFINE) ? p.aff_shift[co] : 0.f;
+      } else if constexpr (EPI) {
+        par[c] = p.coef[n];
+        par[BN + c] = p.coef[p.N + n];
+        par[2 * BN + c] = p.coef[2 * p.N + n];
+      }
+    }
+    vmwait<0>();
+    __syncthreads();
+  }
+
+  // ---- per-lane DMA geometry of a 16 KB A stage: 16 instructions, 2 per wave ----
+  // stage row = ks * 64 + px (ks = 32-deep K step within the chunk)
+  int apx[2], aks[2], apc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 16 + (lane >> 2);
+    aks[i] = row >> 6;
+    apx[i] = row & 63;
+    apc[i] = (lane & 3) ^ (((row >> 2) & 1) << 1);
+  }
+  // tile -> (img, y, x0)
+  auto tile_pos = [&](long t, int& img, int& y, int& x0) {
+    const int tx = (int)(t % p.tiles_x);
+    const long ry = t / p.tiles_x;
+    y = (int)(ry % p.h);
+    img = (int)(ry / p.h);
+    x0 = tx * 64;
+  };
+  const int W2 = 2 * p.w;
+
+  // item q = (tile, chunk); loads: A chunk (+ R tile with the last chunk, EPI)
+  auto issue = [&](long q, int slot) -> int {
+    const long t = t0 + q / nch;
+    const int kc = (int)(q % nch);
+    int img, y, x0;
+    tile_pos(t, img, y, x0);
+    char* S = ring + slot * STAGE;
+    if constexpr (MODE == 0) {
+      const i32x4 rs = rsrc_of((uintptr_t)(p.a + (((size_t)img * p.h + y) * p.w + x0) * p.a_ld + p.a_off + kc * 128));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = x0 + apx[i] < p.w;
+        dma16(ok ? (unsigned)((apx[i] * p.a_ld + aks[i] * 32 + apc[i] * 8) * 2) : OOB, rs, S + (wave * 2 + i) * 1024);
+      }
+    } else {
+      const i32x4 rs = rsrc_of((uintptr_t)(p.a + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.cout));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int k = kc * 128 + aks[i] * 32;  // 32 | cout: the step lies in one tap
+        const int tap = k / p.cout, co = k - tap * p.cout;
+        const bool ok = x0 + apx[i] < p.w;
+        const unsigned off = (unsigned)((((tap >> 1) * W2 + 2 * apx[i] + (tap & 1)) * p.cout + co + apc[i] * 8) * 2);
+        dma16(ok ? off : OOB, rs, S + (wave * 2 + i) * 1024);
+      }
+    }
+    int n = 2;
+    if constexpr (EPI) {
+      if (kc == nch - 1) {  // the producer's r tile [64 px][BN] for the fused BN backward
+        char* R = rr + (int)((q / nch) & 1) * C::RSLOT;
+        const i32x4 rs = rsrc_of((uintptr_t)(p.r + (((size_t)img * p.h + y) * p.w + x0) * p.r_ld + p.r_off + n0));
+        for (int j = wave; j < 64 * PPR / 64; j += 8) {  // 1 KB instructions
+          const int slot16 = j * 64 + lane, px = slot16 / PPR, sl = slot16 - px * PPR;
+          const int pc = sl ^ (px & (PPR - 1));  // piece swizzle by pixel
+          const bool ok = x0 + px < p.w;
+          dma16(ok ? (unsigned)((px * p.r_ld + pc * 8) * 2) : OOB, rs, R + j * 1024);
+        }
+        n += (64 * PPR / 64 + 7 - wave) / 8;
+      }
+    }
+    return n;
+  };
+
+  f32x4 acc[FM][FN];
+  auto zero = [&]() {
+#pragma unroll
+    for (int f = 0; f < FM; ++f)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero();
+
+  auto compute = [&](int slot, int kc) {
+    const char* S = ring + slot * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      uint4 af[FM], bfr[FN];
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+        af[f] = *reinterpret_cast<const uint4*>(S + rsw(ks * 64 + wm * 32 + f * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const uint4*>(
+            Bres + rsw((kc * 4 + ks) * BN + wn * (BN / 4) + j * 16 + (lane & 15), lane >> 4));
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[f][j], bfr[j], af[f]);  // C^T: lanes = pixels
+    }
+  };
+
+  const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE, stats = p.flags & CNNITMO_STATS;
+  // stores per tile epilogue (all issued, out-of-range ones dropped): FM*FN outputs
+  // + MODE 0 stats 2*FN (lanes 0/16/32/48) + EPI sums FN
+  constexpr int SOUT = FM * FN;
+  const int S = SOUT + (MODE == 0 ? (stats ? 2 * FN : 0) : (EPI ? FN : 0));
+  auto epilogue = [&](long t, int rslot) {
+    int img, y, x0;
+    tile_pos(t, img, y, x0);
+    float s1[FN][4], s2[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+    if constexpr (MODE == 0) {
+      const __amdgpu_buffer_rsrc_t os =
+          srsrc(p.out + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.out_ld + p.out_off);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * (BN / 4) + j * 16 + (lane >> 4) * 4;  // first of this lane's 4 columns
+        const int n = n0 + c, tap = n / p.cout, co = n - tap * p.cout;
+        const f32x4_ bj = *reinterpret_cast<const f32x4_*>(par + c);
+        const f32x4_ sj = *reinterpret_cast<const f32x4_*>(par + BN + c);
+        const f32x4_ hj = *reinterpret_cast<const f32x4_*>(par + 2 * BN + c);
+#pragma unroll
+        for (int f = 0; f < FM; ++f) {
+          const int px = wm * 32 + f * 16 + (lane & 15);
+          const bool ok = x0 + px < p.w;
+          bf16 o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[f][j][r] + bj[r];
+            if (relu) v = fmaxf(v, 0.f);
+            if (aff) v = v * sj[r] + hj[r];
+            const float vs = ok ? v : 0.f;
+            s1[j][r] += vs;
+            s2[j][r] += vs * vs;
+            o[r] = from_f32<bf16>(v);
+          }
+          u32x2 pk;
+          __builtin_memcpy(&pk, o, 8);
+          const unsigned off = (unsigned)((((tap >> 1) * W2 + 2 * px + (tap & 1)) * p.out_ld + co) * 2);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, os, ok ? off : OOB, 0, 0);
+        }
+      }
+      if (stats) {
+        const long row = (t * 2 + wm);
+        const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)row * 2 * p.N);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s1[j][r] = row16_sum(s1[j][r]);
+            s2[j][r] = row16_sum(s2[j][r]);
+          }
+          const int n = n0 + wn * (BN / 4) + j * 16 + (lane >> 4) * 4;
+          const f32x4_ a1 = {s1[j][0], s1[j][1], s1[j][2], s1[j][3]};
+          const f32x4_ a2 = {s2[j][0], s2[j][1], s2[j][2], s2[j][3]};
+          const bool w0 = (lane & 15) == 0;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss, w0 ? (unsigned)(n * 4) : OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a2), ss,
+                                                 w0 ? (unsigned)((p.N + n) * 4) : OOB, 0, 0);
+        }
+      }
+    } else {
+      const __amdgpu_buffer_rsrc_t os = srsrc(p.out + (((size_t)img * p.h + y) * p.w + x0) * p.out_ld + p.out_off);
+      const char* R = rr + rslot * C::RSLOT;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * (BN / 4) + j * 16 + (lane >> 4) * 4;
+        f32x4_ ca = {}, cb = {}, ce = {};
+        if constexpr (EPI) {
+          ca = *reinterpret_cast<const f32x4_*>(par + c);
+          cb = *reinterpret_cast<const f32x4_*>(par + BN + c);
+          ce = *reinterpret_cast<const f32x4_*>(par + 2 * BN + c);
+        }
+#pragma unroll
+        for (int f = 0; f < FM; ++f) {
+          const int px = wm * 32 + f * 16 + (lane & 15);
+          const bool ok = x0 + px < p.w;
+          bf16 o[4];
+          if constexpr (EPI) {
+            // r[px][c..c+3]: piece c/8 of row px, stored at piece (c/8) ^ (px & (PPR-1))
+            const bf16* rv = reinterpret_cast<const bf16*>(
+                R + (px * PPR + ((c >> 3) ^ (px & (PPR - 1)))) * 16 + (c & 7) * 2);
+            const uint2 r4 = *reinterpret_cast<const uint2*>(rv);
+            const bf16* rq = reinterpret_cast<const bf16*>(&r4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float gg = to_f32(from_f32<bf16>(acc[f][j][r])), rvv = to_f32(rq[r]);
+              o[r] = from_f32<bf16>(rvv > 0.f ? ca[r] * gg - cb[r] * rvv + ce[r] : 0.f);
+              s1[j][r] += ok ? to_f32(o[r]) : 0.f;
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = from_f32<bf16>(acc[f][j][r]);
+          }
+          u32x2 pk;
+          __builtin_memcpy(&pk, o, 8);
+          __builtin_amdgcn_raw_buffer_store_b64(pk, os, ok ? (unsigned)((px * p.out_ld + n0 + c) * 2) : OOB, 0, 0);
+        }
+      }
+      if constexpr (EPI) {
+        const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)(t * 2 + wm) * p.N);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s1[j][r] = row16_sum(s1[j][r]);
+          const int n = n0 + wn * (BN / 4) + j * 16 + (lane >> 4) * 4;
+          const f32x4_ a1 = {s1[j][0], s1[j][1], s1[j][2], s1[j][3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss,
+                                                 (lane & 15) == 0 ? (unsigned)(n * 4) : OOB, 0, 0);
+        }
+      }
+    }
+    zero();
+  };
+
+  // ---- ST-stage ring over items (tile, chunk); vmcnt counted per wave as in the
+  // halo kernel: retire in issue order, stores included
+  const long T = (t1 - t0) * nch;
+  int issued = 0;
+  int mq[ST];
+#pragma unroll
+  for (int k = 0; k < ST - 1; ++k) {
+    if (k < T) issued += issue(k, k);
+    mq[k] = issued;
+  }
+  mq[ST - 1] = issued;
+  int slot = 0;
+  for (long q = 0; q < T; ++q) {
+    vmwait_dyn(issued - mq[0]);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (q + ST - 1 < T) {
+      issued += issue(q + ST - 1, slot == 0 ? ST - 1 : slot - 1);
+      mq[ST - 1] = issued;
+    }
+    const int kc = (int)(q % nch);
+    compute(slot, kc);
+    if (kc == nch - 1) {
+      epilogue(t0 + q / nch, (int)((q / nch) & 1));
+      issued += S;
+    }
+#pragma unroll
+    for (int k = 0; k < ST - 1; ++k) mq[k] = mq[k + 1];
+    slot = slot == ST - 1 ? 0 : slot + 1;
+  }
+}
+
+struct TSPlan {
+  int bn, st;
+  bool epi;
+};
+
+bool ts_plan(int mode, int h, int w, int cin, int cout, bool epi, TSPlan& pl) {
+  static const int en = [] {
+    const char* e = getenv("CNNITMO_TCONV_STREAM");
+    return e ? atoi(e) : 1;
+  }();
+  if (!en || w < 1 || h < 1) return false;
+  const int K = mode == 0 ? cin : 4 * cout, N = mode == 0 ? 4 * cout : cin;
+  if (K % 128 || cout % 32 || N % 64) return false;
+  int bn = 64 * 1024 / (K * 2);  // the resident weight block: K x BN bf16 <= 64 KB
+  bn = bn >= 256 ? 256 : (bn >= 128 ? 128 : (bn >= 64 ? 64 : 0));
+  while (bn > 64 && N % bn) bn /= 2;
+  if (!bn || N % bn) return false;
+  if (epi && bn > 128) bn = 128;  // LDS: two r slots of 64 x BN
+  // one column block only: with several, every block streams all of A again and
+  // the per-CU LDS-DMA rate (not HBM) becomes the bound (measured slower than the
+  // halo / igemm paths for up6..up8)
+  if (N != bn) return false;
+  pl.bn = bn;
+  pl.epi = epi;
+  if (epi) {
+    if (mode != 1) return false;
+    // the R slot of tile t is refilled with tile t+2's last chunk: 2 * chunks >= ST
+    const int nch = K / 128;
+    pl.st = bn == 64 ? 4 : 3;
+    while (pl.st > 2 && 2 * nch < pl.st) --pl.st;
+    if (2 * nch < pl.st) return false;
+  } else {
+    pl.st = 5;
+  }
+  return true;
+}
+
+template <int MODE, int BN, int ST, bool EPI>
+void ts_launch(const TSArgs& a, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((tconv_stream_kernel<MODE, BN, ST, EPI>), dim3(grid), dim3(512), 0, s, a);
+}
+
+int num_cus() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      ncu = prop.multiProcessorCount;
+    if (ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
+
+}  // namespace
+
+bool tconv_stream_handles(int mode, int h, int w, int cin, int cout, bool epi) {
+  TSPlan pl;
+  return ts_plan(mode, h, w, cin, cout, epi, pl);
+}
+
+long tconv_stream_rows(int n, int h, int w) { return (long)n * h * ((w + 63) / 64) * 2; }
+
+const char* tconv_stream_name(int mode, int h, int w, int cin, int cout, bool epi) {
+  TSPlan pl;
+  if (!ts_plan(mode, h, w, cin, cout, epi, pl)) return "";
+  static thread_local char buf[64];
+  snprintf(buf, sizeof(buf), "tconv_stream_kernel<%d,%d%s>", mode, pl.bn, pl.epi ? ",bnb" : "");
+  return buf;
+}
+
+// mode 0: x [n][h][w] view (x_ld, x_off) -> out [n][2h][2w] view; mode 1: dout -> dx view.
+int launch_tconv_stream(int mode, const void* a, long a_ld, int a_off, const void* b, int n, int h, int w,
+                        int cin, int cout, void* out, long out_ld, int out_off, const float* bias, int flags,
+                        const float* aff_scale, const float* aff_shift, float* stats, const float* coef,
+                        const void* r, long r_ld, int r_off, hipStream_t s, const char* what) {
+  TSPlan pl;
+  const bool epi = coef != nullptr;
+  CNN_REQUIRE(ts_plan(mode, h, w, cin, cout, epi, pl), "%s: no stream plan", what);
+  CNN_REQUIRE(a_ld % 8 == 0 && a_off % 8 == 0 && out_ld % 4 == 0 && out_off % 4 == 0 && (!epi || (r_ld % 8 == 0 && r_off % 8 == 0)),
+              "%s: misaligned views", what);
+  TSArgs t;
+  t.a = (const bf16*)a; t.a_ld = a_ld; t.a_off = a_off; t.b = (const bf16*)b;
+  t.nimg = n; t.h = h; t.w = w; t.cout = cout;
+  t.K = mode == 0 ? cin : 4 * cout;
+  t.N = mode == 0 ? 4 * cout : cin;
+  t.nblocks = t.N / pl.bn;
+  t.tiles_x = (w + 63) / 64;
+  t.ntiles = (long)n * h * t.tiles_x;
+  t.out = (bf16*)out; t.out_ld = out_ld; t.out_off = out_off;
+  t.bias = bias; t.flags = flags; t.aff_scale = aff_scale; t.aff_shift = aff_shift; t.stats = stats;
+  t.coef = coef; t.r = (const bf16*)r; t.r_ld = r_ld; t.r_off = r_off;
+  CNN_REQUIRE(!(flags & CNNITMO_STATS) || stats, "%s: STATS without buffer", what);
+  CNN_REQUIRE(!epi || stats, "%s: fused BN backward without a sums buffer", what);
+  // 8 | grid and nblocks | grid / 8 (XCD-aware mapping in the kernel)
+  const int per_xcd = std::max(t.nblocks, num_cus() / 8 / t.nblocks * t.nblocks);
+  const int grid = 8 * per_xcd;
+#define L1(M, B, S, E) ts_launch<M, B, S, E>(t, grid, s)
+  if (mode == 0) {
+    if (pl.bn == 256) L1(0, 256, 5, false);
+    else if (pl.bn == 128) L1(0, 128, 5, false);
+    else L1(0, 64, 5, false);
+  } else if (!epi) {
+    if (pl.bn == 256) L1(1, 256, 5, false);
+    else if (pl.bn == 128) L1(1, 128, 5, false);
+    else L1(1, 64, 5, false);
+  } else {
+    if (pl.bn == 128) {
+      if (pl.st == 3) L1(1, 128, 3, true);
+      else L1(1, 128, 2, true);
+    } else if (pl.bn == 64) {
+      if (pl.st == 4) L1(1, 64, 4, true);
+      else if (pl.st == 3) L1(1, 64, 3, true);
+      else L1(1, 64, 2, true);
+    } else {
+      cnnitmo_set_error("%s: fused BN backward needs BN <= 128", what);
+      return CNNITMO_EUNSUPPORTED;
+    }
+  }
+#undef L1
+  return cnnitmo_check_launch(what);
+}

@@ -347,12 +347,17 @@ class BlockStage(Stage):
         """The (value, channel offset) among `targets` whose BN backward this stage's dgrad
         applies (cnnitmo_conv3x3_dgrad_bn), with its partial-sum row count; or None."""
         e = self.eng
-        if self.kind != "c3" or not e.fuse_bnb or not self.vin.needs_grad:
+        if self.kind not in ("c3", "t2") or not e.fuse_bnb or not self.vin.needs_grad:
             return None
         for m, ci0 in targets:
             if m.fuse_into is self and m.sum_consumers == 1:
-                rows = ops.conv3x3_dgrad_bn_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, self.cin, ci0,
-                                                 ci0 + m.c)
+                if self.kind == "c3":
+                    rows = ops.conv3x3_dgrad_bn_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, self.cin, ci0,
+                                                     ci0 + m.c)
+                elif ci0 == 0 and m.c == self.cin and m.producer.kind != "t2":  # (no parity sums here)
+                    rows = ops.tconv_dgrad_bn_rows(e.dt, n, self.vin.h, self.vin.w, self.cout, self.cin)
+                else:
+                    rows = 0
                 if rows > 0:
                     return m, ci0, rows
         return None
@@ -417,10 +422,15 @@ class BlockStage(Stage):
                 self.vin.ensure_grad(n, e.tdtype, e.device)
                 dx = self.vin.gview(n)
             ppar = prod.fold_active and prod.kind == "t2"
-            dzp = torch.empty(P * m.c, dtype=e.tdtype, device=e.device)
+            pin = n * self.vin.h * self.vin.w
+            dzp = torch.empty(pin * m.c, dtype=e.tdtype, device=e.device)
             pp = torch.empty(frows * (4 if ppar else 1) * m.c, device=e.device, dtype=torch.float32)
-            ops.conv3x3_dgrad_bn(e.dt, dz, n, self.vout.h, self.vout.w, cout, self.w_bwd, self.cin, dx, ci0,
-                                 ci0 + m.c, coef, prod.r, dzp, pp, ppar)
+            if self.kind == "c3":
+                ops.conv3x3_dgrad_bn(e.dt, dz, n, self.vout.h, self.vout.w, cout, self.w_bwd, self.cin, dx, ci0,
+                                     ci0 + m.c, coef, prod.r, dzp, pp, ppar)
+            else:
+                ops.tconv_dgrad_bn(e.dt, dz, n, self.vin.h, self.vin.w, cout, self.w_bwd, self.cin, coef, prod.r,
+                                   dzp, pp)
             prod.fused = (dzp, pp, frows)
             if not whole:
                 if self.vin.place:
@@ -654,8 +664,8 @@ def _plan_bn_sums(stages):
             (isinstance(r, BlockStage) and r.kind in ("c3", "t2")) or isinstance(r, (PoolStage, HeadStage))
             for r in rs)
         v.sum_consumers = len(rs) if ok else 0
-        v.fuse_into = rs[0] if (ok and len(rs) == 1 and isinstance(rs[0], BlockStage) and rs[0].kind == "c3") \
-            else None
+        v.fuse_into = rs[0] if (ok and len(rs) == 1 and isinstance(rs[0], BlockStage) and
+                                rs[0].kind in ("c3", "t2")) else None
 
 
 def layout_params(stages):

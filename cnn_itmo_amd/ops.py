@@ -102,6 +102,17 @@ def conv3x3_dgrad_bn(dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1, coef, r, dz_
          c0, c1, ptr(coef), rp, rld, roff, ptr(dz_out), ptr(part), 1 if parity else 0, stream_ptr())
 
 
+def tconv_dgrad_bn_rows(dt, n, h, w, cout, cin):
+    return query("cnnitmo_tconv2x2_dgrad_bn_rows", dt, n, h, w, cout, cin)
+
+
+def tconv_dgrad_bn(dt, dout, n, h, w, cout, kT, cin, coef, r, dz_out, part):
+    """tconv2x2_dgrad with the producer's BN backward fused (see cnn_itmo.h)."""
+    rp, rld, roff = _rview(r, cin)
+    call("cnnitmo_tconv2x2_dgrad_bn", dt, ptr(dout), n, h, w, cout, ptr(kT), cin, ptr(coef), rp, rld, roff,
+         ptr(dz_out), ptr(part), stream_ptr())
+
+
 def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0, fold=None, raw=None):
     """fold = (scale, shift, db, border_sums) for a folded input BN, else None;
     raw (optional, dw-shaped fp32): the uncorrected dz (x) r sum."""

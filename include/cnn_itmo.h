@@ -160,6 +160,16 @@ int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int w, int cin,
  * kT: [cin][2][2][cout] (from cnnitmo_prep_tconv2x2_weights). */
 int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h, int w, int cout,
                            const void* kT, int cin, void* dx, void* stream);
+/* tconv2x2_dgrad with the PRODUCER's BN backward fused into its store (bf16;
+ * the tconv input is a folded BN output whose coefficients coef [3][cin] are
+ * known): dz_out [n*h*w][cin] = [r>0]*(a*g - b*r + e) of the input gradient g,
+ * r the producer's saved view (element (p, c) at r[p*r_ld + r_off + c]), and
+ * column-sum partials part [rows][cin] (rows = cnnitmo_tconv2x2_dgrad_bn_rows;
+ * 0 = not available for these sizes).  Replaces tconv2x2_dgrad + bn_bwd_apply. */
+long cnnitmo_tconv2x2_dgrad_bn_rows(int dtype, int n, int h, int w, int cout, int cin);
+int cnnitmo_tconv2x2_dgrad_bn(int dtype, const void* dout, int n, int h, int w, int cout,
+                              const void* kT, int cin, const float* coef, const void* r, int r_ld,
+                              int r_off, void* dz_out, float* part, void* stream);
 /* dk [2][2][cout][cin] fp32 (OVERWRITTEN) from x [n,h,w,cin], dout [n,2h,2w,cout]. */
 int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h, int w,
                            int cin, int cout, float* dk, const float* fold_scale,

@@ -304,3 +304,41 @@ def test_conv3x3_dgrad_bn_fused(cin, cout, H, W, c0, c1, par):
         gr = host(g).reshape(P, cin)
         assert np.array_equal(gx[:, :c0], gr[:, :c0]) and np.array_equal(gx[:, c1:], gr[:, c1:])
         assert float(np.abs(gx[:, c0:c1]).max()) == 0.0  # fused columns are not written to dx
+
+
+@pytest.mark.parametrize("cin,cout,H,W", [(128, 64, 3, 70), (64, 32, 4, 64), (128, 32, 2, 130)])
+def test_tconv_dgrad_bn_fused(cin, cout, H, W):
+    """cnnitmo_tconv2x2_dgrad_bn == tconv2x2_dgrad followed by bn_bwd_apply (r from a view)."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin + W)
+    N, d = 2, DT["bf16"]
+    k = (rng.standard_normal((2, 2, cout, cin)) * 0.1).astype(np.float32)
+    kf = torch.empty(k.size, dtype=torch.bfloat16, device="cuda")
+    kT = torch.empty(k.size, dtype=torch.bfloat16, device="cuda")
+    ops.prep_tconv(d, torch.tensor(k).cuda(), cout, cin, kf, kT)
+    dout = dev(rng.standard_normal((N, 2 * H, 2 * W, cout)).astype(np.float32), "bf16").reshape(-1)
+    ld, off = cin + 32, 32
+    rb = dev(np.maximum(rng.standard_normal((N, H, W, ld)), 0).astype(np.float32), "bf16").reshape(-1)
+    rv = ops.View(rb, N, H, W, cin, ld, off)
+    coef = cu(rng.standard_normal(3 * cin).astype(np.float32))
+    P = N * H * W
+    g = torch.empty(P * cin, dtype=torch.bfloat16, device="cuda")
+    ops.tconv_dgrad(d, dout, N, H, W, cout, kT, cin, g)
+    rows = ops.bn_bwd_rows(P, cin)
+    pref = torch.empty(rows * cin, device="cuda")
+    zref = torch.empty(P * cin, dtype=torch.bfloat16, device="cuda")
+    ops.bn_bwd_apply(d, ops.View(g, N, H, W, cin, cin), rv, cin, coef, 0, 0, 0, zref, pref)
+    sref = torch.empty(cin, device="cuda")
+    ops.colsum(pref, rows, cin, 1, sref)
+    frows = ops.tconv_dgrad_bn_rows(d, N, H, W, cout, cin)
+    assert frows > 0
+    zf = torch.empty(P * cin, dtype=torch.bfloat16, device="cuda")
+    pf = torch.empty(frows * cin, device="cuda")
+    ops.tconv_dgrad_bn(d, dout, N, H, W, cout, kT, cin, coef, rv, zf, pf)
+    sf = torch.empty(cin, device="cuda")
+    ops.colsum(pf, frows, cin, 1, sf)
+    torch.cuda.synchronize()
+    a, b = host(zf), host(zref)
+    assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())
+    assert np.mean(a != b) < 1e-3
+    np.testing.assert_allclose(host(sf), host(sref), rtol=1e-4, atol=1e-2)
