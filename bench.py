@@ -86,8 +86,9 @@ class KernelTimer:
 
     def _wrap(self):
         ops = self.ops
-        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_dgrad", "tconv_fwd", "tconv_dgrad",
-                                           "conv1tap_fwd", "conv_wgrad", "tconv_wgrad")}
+        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
+                                           "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
+                                           "tconv_wgrad")}
 
         def kname(dt, n, h, w, cin, cout, dgrad):
             return ops.query("cnnitmo_conv3x3_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
@@ -101,6 +102,17 @@ class KernelTimer:
             fl = 2.0 * n * h * w * cin * 9 * cout
             return self._bracket(kname(dt, n, h, w, cin, cout, 1), fl, o["conv3x3_dgrad"], dt, dz, n, h, w, cout,
                                  wflip, cin, dx)
+
+        def conv3x3_dgrad_bn(dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1, *a, **k):
+            fl = 2.0 * n * h * w * cin * 9 * cout
+            name = ops.query("cnnitmo_conv3x3_dgrad_bn_kernel_name", dt, n, h, w, cout, cin, c0, c1).decode()
+            return self._bracket(name, fl, o["conv3x3_dgrad_bn"], dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1,
+                                 *a, **k)
+
+        def tconv_dgrad_bn(dt, dout, n, h, w, cout, kT, cin, *a, **k):
+            fl = 2.0 * n * h * w * cin * 4 * cout
+            name = ops.query("cnnitmo_tconv2x2_dgrad_bn_kernel_name", dt, n, h, w, cout, cin).decode()
+            return self._bracket(name, fl, o["tconv_dgrad_bn"], dt, dout, n, h, w, cout, kT, cin, *a, **k)
 
         def tname(dt, n, h, w, cin, cout, dgrad):
             return ops.query("cnnitmo_tconv2x2_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
@@ -133,8 +145,9 @@ class KernelTimer:
             return self._bracket(wname(dt, 4, x.n, x.h, x.w, x.c, cout), fl, o["tconv_wgrad"],
                                  dt, x, dout, cout, dk, *a, **k)
 
-        for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad), ("tconv_fwd", tconv_fwd),
-                     ("tconv_dgrad", tconv_dgrad), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),
+        for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad),
+                     ("conv3x3_dgrad_bn", conv3x3_dgrad_bn), ("tconv_fwd", tconv_fwd),
+                     ("tconv_dgrad", tconv_dgrad), ("tconv_dgrad_bn", tconv_dgrad_bn), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),
                      ("tconv_wgrad", tconv_wgrad)):
             setattr(ops, n, f)
 

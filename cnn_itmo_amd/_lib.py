@@ -81,6 +81,8 @@ SIGNATURES = {
     "cnnitmo_conv3x3_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_wgrad_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_tconv2x2_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32, i32]),
+    "cnnitmo_conv3x3_dgrad_bn_kernel_name": (C.c_char_p, [i32] * 8),
+    "cnnitmo_tconv2x2_dgrad_bn_kernel_name": (C.c_char_p, [i32] * 6),
     "cnnitmo_border_sums": (i32, [i32, vp, i32, i32, i32, i32, vp, vp]),
     "cnnitmo_rmsprop": (i32, [vp, vp, vp, i64, f32, f32, f32, f32, vp]),
 }

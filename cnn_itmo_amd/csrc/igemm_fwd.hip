@@ -469,6 +469,15 @@ extern "C" long cnnitmo_conv3x3_dgrad_bn_rows(int dtype, int n, int h, int w, in
   return halo_stat_rows(a);
 }
 
+// Name of the kernel cnnitmo_conv3x3_dgrad_bn launches for these sizes (for profiles).
+extern "C" const char* cnnitmo_conv3x3_dgrad_bn_kernel_name(int dtype, int n, int h, int w, int cout, int cin,
+                                                            int c0, int c1) {
+  FwdArgs a = dgrad_bn_args(n, h, w, cout, cin);
+  a.bnb_c0 = c0; a.bnb_c1 = c1; a.bnb_out = (void*)1; a.bnb_r_ld = 8;
+  if (dtype != CNNITMO_BF16 || !halo_handles(a)) return "";
+  return halo_name(a);
+}
+
 extern "C" int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h, int w, int cout,
                                         const void* wt_flip, int cin, void* dx, int dx_ld, int dx_off,
                                         int c0, int c1, const float* coef, const void* r, int r_ld,
@@ -525,6 +534,13 @@ extern "C" int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h,
 extern "C" long cnnitmo_tconv2x2_dgrad_bn_rows(int dtype, int n, int h, int w, int cout, int cin) {
   if (dtype != CNNITMO_BF16 || !tconv_stream_handles(1, h, w, cin, cout, true)) return 0;
   return tconv_stream_rows(n, h, w);
+}
+
+// Name of the kernel cnnitmo_tconv2x2_dgrad_bn launches for these sizes (for profiles).
+extern "C" const char* cnnitmo_tconv2x2_dgrad_bn_kernel_name(int dtype, int n, int h, int w, int cout, int cin) {
+  (void)n;
+  if (dtype != CNNITMO_BF16 || !tconv_stream_handles(1, h, w, cin, cout, true)) return "";
+  return tconv_stream_name(1, h, w, cin, cout, true);
 }
 
 extern "C" int cnnitmo_tconv2x2_dgrad_bn(int dtype, const void* dout, int n, int h, int w, int cout,

@@ -113,6 +113,9 @@ int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h, int w, int
                              const void* wt_flip, int cin, void* dx, int dx_ld, int dx_off, int c0,
                              int c1, const float* coef, const void* r, int r_ld, int r_off,
                              void* dz_out, float* part, int parity, void* stream);
+/* Label of the kernel cnnitmo_conv3x3_dgrad_bn launches ("" = unavailable; profiling only). */
+const char* cnnitmo_conv3x3_dgrad_bn_kernel_name(int dtype, int n, int h, int w, int cout, int cin,
+                                                 int c0, int c1);
 
 /* Weight-gradient of conv3x3 (TF Conv2DBackpropFilter).  x view [n,h,w,cin];
  * dz [n,h,w,cout] contiguous; dw: [cout][3][3][cin] fp32, OVERWRITTEN.
@@ -170,6 +173,8 @@ long cnnitmo_tconv2x2_dgrad_bn_rows(int dtype, int n, int h, int w, int cout, in
 int cnnitmo_tconv2x2_dgrad_bn(int dtype, const void* dout, int n, int h, int w, int cout,
                               const void* kT, int cin, const float* coef, const void* r, int r_ld,
                               int r_off, void* dz_out, float* part, void* stream);
+/* Label of the kernel cnnitmo_tconv2x2_dgrad_bn launches ("" = unavailable; profiling only). */
+const char* cnnitmo_tconv2x2_dgrad_bn_kernel_name(int dtype, int n, int h, int w, int cout, int cin);
 /* dk [2][2][cout][cin] fp32 (OVERWRITTEN) from x [n,h,w,cin], dout [n,2h,2w,cout]. */
 int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h, int w,
                            int cin, int cout, float* dk, const float* fold_scale,
