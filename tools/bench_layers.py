@@ -87,6 +87,18 @@ def main():
             if "dgrad" in want:
                 dx = ops.new_view(B, h, w, cin, T)
                 rows.append((name, "dgrad", fl, timeit(lambda: ops.conv3x3_dgrad(dt, out.buf, B, h, w, cout, wt, cin, dx), a.iters)))
+            if "dgradbn" in want and name.startswith("dec"):
+                # decoder dgrad with the up-path producer's BN backward fused (engine: concat
+                # [skip, up], up = the tconv output at channels [cin - cout, cin), parity sums)
+                c0, c1 = cin - cout, cin
+                dx = ops.new_view(B, h, w, cin, T)
+                r = ops.View(x.buf, B, h, w, cout, cin, c0)
+                coef = torch.rand(3 * cout, device="cuda")
+                rows_ = ops.conv3x3_dgrad_bn_rows(dt, B, h, w, cout, cin, c0, c1)
+                dzp = torch.empty(B * h * w * cout, dtype=T, device="cuda")
+                pp = torch.empty(rows_ * 4 * cout, device="cuda")
+                rows.append((name, "dgradbn", fl, timeit(lambda: ops.conv3x3_dgrad_bn(
+                    dt, out.buf, B, h, w, cout, wt, cin, dx, c0, c1, coef, r, dzp, pp, True), a.iters)))
             if "wgrad" in want:
                 dw = torch.empty(cout * 9 * cin, device="cuda", dtype=torch.float32)
                 rows.append((name, "wgrad", fl, timeit(lambda: ops.conv_wgrad(dt, 9, x, out.buf, cout, dw), a.iters)))

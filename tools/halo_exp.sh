@@ -21,6 +21,6 @@ else
   for n in 0 1 2 3 4 5 6 7 7; do
     lib="$R/cnn_itmo_amd/lib/libcnnitmo.so"; [ $n -gt 0 ] && lib="$R/exp/libcnnitmo_exp$n.so"
     echo "== HALO_EXP=$n"
-    CNNITMO_LIB=$lib timeout -k 10 120 python "$R/tools/bench_layers.py" --layers "$L" --ops fwd,dgrad --iters 5 | grep -E "fwd|dgrad"
+    CNNITMO_LIB=$lib timeout -k 10 120 python "$R/tools/bench_layers.py" --layers "$L" --ops ${OPS:-fwd,dgrad} --iters 5 | grep -E "fwd|dgrad"
   done
 fi
