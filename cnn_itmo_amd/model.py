@@ -166,8 +166,15 @@ class Model:
             pending = getattr(self, "_pending_accum", None)
             if pending is not None:
                 import torch
-                self.engine.accum.copy_(torch.as_tensor(pending[0]))
-                self.engine.step = pending[1]
+                if pending[0] == "named":  # per-tensor accumulators (Keras HDF5 optimizer_weights)
+                    for k, v in pending[1].items():
+                        off, shp = self.engine.pslices[k]
+                        self.engine.accum[off:off + int(np.prod(shp))].copy_(
+                            torch.as_tensor(np.ascontiguousarray(v, np.float32).reshape(-1)))
+                    self.engine.step = pending[2]
+                else:
+                    self.engine.accum.copy_(torch.as_tensor(pending[0]))
+                    self.engine.step = pending[1]
                 self._pending_accum = None
         return self.engine
 
@@ -311,9 +318,30 @@ class Model:
         return {"name": self.name, "layers": nodes, "input": self.inputs[0].layer.name,
                 "output": self.outputs[0].layer.name}
 
+    def named_accumulators(self):
+        """RMSprop accumulators per trainable weight (internal layout), or None before
+        the first step / without an optimizer state."""
+        pending = getattr(self, "_pending_accum", None)
+        if self.engine is None:
+            if pending is not None and pending[0] == "named":
+                return {k: v.copy() for k, v in pending[1].items()}
+            return None
+        acc = self.engine.accum.cpu().numpy()
+        return {k: acc[off:off + int(np.prod(shp))].reshape(shp).copy()
+                for k, (off, shp) in self.engine.pslices.items()}
+
+    @staticmethod
+    def _is_h5_path(path):
+        return str(path).lower().endswith((".h5", ".hdf5", ".keras", ".hdf"))
+
     def save(self, path, include_optimizer=True):
-        """Architecture + weights (+ RMSprop accumulators) in one .npz (the role of
-        ModelCheckpoint's HDF5, main.py:124)."""
+        """``*.h5`` / ``*.hdf5``: the Keras 2.2 HDF5 layout the reference's ModelCheckpoint
+        writes (main.py:124; keras_h5.py).  Any other path: architecture + weights
+        (+ RMSprop accumulators) in one .npz."""
+        if self._is_h5_path(path):
+            from . import keras_h5
+            keras_h5.save_model_hdf5(self, path, include_optimizer=include_optimizer)
+            return
         arrays = {"__config__": np.frombuffer(json.dumps(self.get_config()).encode(), np.uint8)}
         for k, v in self.named_weights().items():
             arrays["w/" + k] = v
@@ -328,15 +356,29 @@ class Model:
         os.replace(tmp, path)
 
     def save_weights(self, path):
+        if self._is_h5_path(path):
+            from . import keras_h5
+            keras_h5.save_model_hdf5(self, path, weights_only=True)
+            return
         self.save(path, include_optimizer=False)
 
     def load_weights(self, path):
+        from . import hdf5
+        if hdf5.is_hdf5(path):
+            from . import keras_h5
+            keras_h5.load_weights_hdf5(self, path)
+            return
         with np.load(path, allow_pickle=False) as z:
             self.set_named_weights({k[2:]: z[k] for k in z.files if k.startswith("w/")})
 
 
 def load_model(path, compile=True):
-    """keras.models.load_model (predict.py:24) for files written by Model.save."""
+    """keras.models.load_model (predict.py:24): a Keras 2.2 HDF5 model file (as the
+    reference's ModelCheckpoint writes it) or an .npz written by Model.save."""
+    from . import hdf5
+    if hdf5.is_hdf5(path):
+        from . import keras_h5
+        return keras_h5.load_model_hdf5(path, compile=compile)
     from . import layers as Lm
     with np.load(path, allow_pickle=False) as z:
         cfg = json.loads(bytes(z["__config__"]).decode())
