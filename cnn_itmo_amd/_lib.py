@@ -35,6 +35,7 @@ sz = C.c_size_t
 SIGNATURES = {
     "cnnitmo_version": (i32, []),
     "cnnitmo_last_error": (C.c_char_p, []),
+    "cnnitmo_augment_affine": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, f32, vp, vp]),
     "cnnitmo_conv3x3_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp]),
     "cnnitmo_fwd_stat_rows": (i32, [i32, i64, i32]),
     "cnnitmo_tconv2x2_dgrad_bn_rows": (i64, [i32, i32, i32, i32, i32, i32]),

@@ -184,7 +184,10 @@ class Model:
 
     # ---- inference -------------------------------------------------------------
     def _to_dev(self, x):
+        """Host arrays are copied in; CUDA tensors (e.g. datagen batches) are used as they are."""
         import torch
+        if isinstance(x, torch.Tensor):
+            return x.float().cuda() if not x.is_cuda else x.float()
         return torch.as_tensor(np.asarray(x, dtype=np.float32)).cuda()
 
     def predict(self, x, batch_size=32, verbose=0, steps=None):

@@ -296,3 +296,13 @@ def pool_bnsums(dt, dyp, idx, r: View, mean, inv, part):
 
 def rmsprop(p, g, a, lr, rho, eps, grad_scale=1.0):
     call("cnnitmo_rmsprop", ptr(p), ptr(g), ptr(a), p.numel(), lr, rho, eps, grad_scale, stream_ptr())
+
+
+def augment_affine(src, mats, flips, scale, dst):
+    """src [n,h,w,c] uint8/fp32 device tensor; mats [n,6] fp64 and flips [n] int32 device
+    tensors; dst [n,h,w,c] fp32 (cnnitmo_augment_affine)."""
+    n, h, w, c = src.shape
+    assert src.is_contiguous() and dst.is_contiguous() and tuple(dst.shape) == (n, h, w, c)
+    assert mats.dtype == torch.float64 and flips.dtype == torch.int32 and mats.numel() == 6 * n
+    call("cnnitmo_augment_affine", 1 if src.dtype == torch.uint8 else 0, ptr(src), n, h, w, c, ptr(mats),
+         ptr(flips), float(scale), ptr(dst), stream_ptr())

@@ -327,6 +327,20 @@ int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
 int cnnitmo_rmsprop(float* p, const float* g, float* a, long n, float lr, float rho, float eps,
                     float grad_scale, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Training-data augmentation -- replaces the paired keras ImageDataGenerator
+ * (rescale, rotation_range, horizontal/vertical_flip, zoom_range;
+ * /root/reference/main.py:71-77 -> keras_preprocessing apply_transform +
+ * standardize).  src [n,h,w,c] uint8 (src_u8 = 1) or fp32; mats [n][6] fp64 =
+ * (a00, a01, t0, a10, a11, t1) mapping an output (row, col) to the input
+ * (row, col) (transform_matrix_offset_center(rotation @ zoom)); flips [n]
+ * (bit 0 horizontal, bit 1 vertical, applied after the affine map); bilinear
+ * with clamp-to-edge ('nearest' fill, scipy order 1); dst [n,h,w,c] fp32 =
+ * float32(interpolated) * scale.  c = 1 or 3.
+ */
+int cnnitmo_augment_affine(int src_u8, const void* src, int n, int h, int w, int c, const double* mats,
+                           const int* flips, float scale, float* dst, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
