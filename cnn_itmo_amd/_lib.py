@@ -36,6 +36,10 @@ SIGNATURES = {
     "cnnitmo_version": (i32, []),
     "cnnitmo_last_error": (C.c_char_p, []),
     "cnnitmo_augment_affine": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, f32, vp, vp]),
+    "cnnitmo_tonemap_workspace_bytes": (sz, [i32]),
+    "cnnitmo_tonemap_stats": (i32, [i32, vp, i32, i32, i32, vp, vp, vp, sz, vp]),
+    "cnnitmo_tonemap_apply": (i32, [i32, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
+    "cnnitmo_inverse_reinhard_apply": (i32, [i32, vp, i32, i32, i32, vp, vp, f64, f64, vp, vp]),
     "cnnitmo_conv3x3_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp]),
     "cnnitmo_fwd_stat_rows": (i32, [i32, i64, i32]),
     "cnnitmo_tconv2x2_dgrad_bn_rows": (i64, [i32, i32, i32, i32, i32, i32]),

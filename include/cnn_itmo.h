@@ -341,6 +341,30 @@ int cnnitmo_rmsprop(float* p, const float* g, float* a, long n, float lr, float 
 int cnnitmo_augment_affine(int src_u8, const void* src, int n, int h, int w, int c, const double* mats,
                            const int* flips, float scale, float* dst, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * Dataset generation / HDR reconstruction maps -- replace the reference's
+ * MATLAB scripts m-files/Reinhard.m:10-24 (tone mapping of HDR crops into the
+ * SDR training inputs), m-files/virtual_camera.m:10-31 (random exposure + camera
+ * curve) and m-files/inverse_Reinhard.m:1-23 (SDR -> HDR), float64 arithmetic.
+ * Images are NHWC RGB: HDR fp32, SDR uint8.  lum_coef: HOST pointer to the 3
+ * luminance weights of RGB2Lum (not in the reference; NULL = Rec. 709).
+ *   stats (device, [n][2]) = per image: sum of log(max(f, realmin)) over pixels,
+ *   and the count of zero-luminance pixels; f = Y (mode 0, fp32 HDR input) or
+ *   X = I/(I-1) (mode 1, uint8 SDR, inverse_Reinhard.m as written).
+ *   apply: curve 0 = Reinhard, 1 = virtual camera; params (device, [n][3]) =
+ *   (key*2^v, n, y) -- Reinhard uses (0.18, -, -); out fp32 or, out_u8 = 1,
+ *   imwrite's uint8(255*x).  inverse: a = the key (0.18); mode 1 = the script
+ *   (uint8 sdr, stats of mode 1, g unused); mode 2 = the exact inverse of
+ *   Reinhard.m for a linear fp32 sdr and the HDR log-average g (stats unused).
+ */
+size_t cnnitmo_tonemap_workspace_bytes(int n);
+int cnnitmo_tonemap_stats(int mode, const void* img, int n, int h, int w, const double* lum_coef,
+                          double* stats, void* workspace, size_t ws_bytes, void* stream);
+int cnnitmo_tonemap_apply(int curve, const float* hdr, int n, int h, int w, const double* lum_coef,
+                          const double* params, const double* stats, int out_u8, void* out, void* stream);
+int cnnitmo_inverse_reinhard_apply(int mode, const void* sdr, int n, int h, int w, const double* lum_coef,
+                                   const double* stats, double a, double g, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
