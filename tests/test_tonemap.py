@@ -105,4 +105,5 @@ def test_gpu_exact_roundtrip_full_hd(gpu):
     G = gpu.log_average(hdr).cpu().numpy()
     for i in range(2):
         back = gpu.inverse_reinhard(sdr[i:i + 1], mode="exact", g=float(G[i]))[0].cpu().numpy()
-        np.testing.assert_allclose(back, hdr[i], rtol=5e-6)
+        # the fp32 SDR in between limits it: X = L/(1-L) amplifies L's rounding by 1/(1-L)
+        np.testing.assert_allclose(back, hdr[i], rtol=3e-5)
