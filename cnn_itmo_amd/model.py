@@ -166,7 +166,7 @@ class Model:
             pending = getattr(self, "_pending_accum", None)
             if pending is not None:
                 import torch
-                if pending[0] == "named":  # per-tensor accumulators (Keras HDF5 optimizer_weights)
+                if isinstance(pending[0], str):  # ("named", {key: array}, step): per-tensor accumulators (Keras HDF5 optimizer_weights)
                     for k, v in pending[1].items():
                         off, shp = self.engine.pslices[k]
                         self.engine.accum[off:off + int(np.prod(shp))].copy_(
@@ -326,7 +326,7 @@ class Model:
         the first step / without an optimizer state."""
         pending = getattr(self, "_pending_accum", None)
         if self.engine is None:
-            if pending is not None and pending[0] == "named":
+            if pending is not None and isinstance(pending[0], str):
                 return {k: v.copy() for k, v in pending[1].items()}
             return None
         acc = self.engine.accum.cpu().numpy()

@@ -231,6 +231,28 @@ def test_save_load_roundtrip(tmp_path):
     assert m2.count_params() == m.count_params()
 
 
+@pytest.mark.parametrize("ext", ["npz", "hdf5"])
+def test_checkpoint_resume_is_exact(tmp_path, ext):
+    """ModelCheckpoint -> load_model -> continue training == uninterrupted training
+    (weights, BN moving stats and RMSprop accumulators all round-trip)."""
+    import cnn_itmo_amd as C
+    rng = np.random.default_rng(3)
+    x = rng.uniform(size=(2, 32, 32, 3))
+    t = rng.uniform(size=x.shape)
+    m = build_unet((32, 32, 3), "float32", seed=4)
+    m.train_on_batch(x, t)
+    p = str(tmp_path / f"saved7-model-01-0.50.{ext}")
+    m.save(p)
+    m.train_on_batch(x, t)
+    C.clear_session()
+    m2 = C.load_model(p)
+    m2._engine().step = m._engine().step - 1  # dropout seed follows the step counter
+    m2.train_on_batch(x, t)
+    a, b = m.named_weights(), m2.named_weights()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
 def test_fit_generator_loss_decreases():
     """main.py:126-132 shape of use: fit_generator over a paired generator."""
     rng = np.random.default_rng(9)
