@@ -88,7 +88,7 @@ class KernelTimer:
         ops = self.ops
         o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
                                            "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
-                                           "tconv_wgrad")}
+                                           "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad")}
 
         def kname(dt, n, h, w, cin, cout, dgrad):
             return ops.query("cnnitmo_conv3x3_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
@@ -131,6 +131,14 @@ class KernelTimer:
             fl = 2.0 * m * out.c * 27  # algorithmic K = 3x3x3 (the packed 32 has 5 zero columns)
             return self._bracket(self.fwd_name(dt, out.c), fl, o["conv1tap_fwd"], dt, cols, kk, m, wt, bias, out, *a, **k)
 
+        def conv_c3_fwd(x, n, hv, h, w, *a, **k):
+            fl = 2.0 * n * h * w * 32 * 27
+            return self._bracket("conv_c3_fwd_kernel", fl, o["conv_c3_fwd"], x, n, hv, h, w, *a, **k)
+
+        def conv_c3_wgrad(x, n, hv, h, w, *a, **k):
+            fl = 2.0 * n * h * w * 32 * 27
+            return self._bracket("conv_c3_wgrad_kernel + fold", fl, o["conv_c3_wgrad"], x, n, hv, h, w, *a, **k)
+
         def wname(dt, ntaps, n, h, w, cin, cout):
             k = ops.query("cnnitmo_wgrad_kernel_name", dt, ntaps, n, h, w, cin, cout).decode()
             return k + " + slab_reduce"
@@ -148,7 +156,7 @@ class KernelTimer:
         for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad),
                      ("conv3x3_dgrad_bn", conv3x3_dgrad_bn), ("tconv_fwd", tconv_fwd),
                      ("tconv_dgrad", tconv_dgrad), ("tconv_dgrad_bn", tconv_dgrad_bn), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),
-                     ("tconv_wgrad", tconv_wgrad)):
+                     ("tconv_wgrad", tconv_wgrad), ("conv_c3_fwd", conv_c3_fwd), ("conv_c3_wgrad", conv_c3_wgrad)):
             setattr(ops, n, f)
 
     def summary(self):

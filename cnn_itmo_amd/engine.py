@@ -161,6 +161,9 @@ class BlockStage(Stage):
             self.w_fwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
             self.w_bwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
         self.foldable = self.kind != "c3in" and self.vin.folded
+        # first layer without im2col (bf16, 32 filters; CNNITMO_C3_DIRECT=0: im2col + 1-tap GEMM)
+        self.direct = (self.kind == "c3in" and eng.dt == L.BF16 and cout == 32
+                       and os.environ.get("CNNITMO_C3_DIRECT", "1") != "0")
         if self.foldable:  # per-step folded copies (training)
             f32 = torch.float32
             self.w_fold = torch.empty_like(self.w_fwd)
@@ -199,6 +202,9 @@ class BlockStage(Stage):
             return
         if self.kind == "c3":
             ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
+        elif self.kind == "c3in" and self.direct:
+            ops.conv_c3_fwd(e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.w_fwd, bias, out_view, flags,
+                            aff, stats)
         elif self.kind == "c3in":
             ops.conv1tap_fwd(e.dt, self.cols, 32, n * self.vout.h * self.vout.w, self.w_fwd, bias,
                              out_view, flags, aff, stats)
@@ -226,7 +232,7 @@ class BlockStage(Stage):
         cout = self.cout
         P = n * self.vout.h * self.vout.w
         self.fold_active = training and self.foldable
-        if self.kind == "c3in":
+        if self.kind == "c3in" and not self.direct:
             self.cols = torch.empty(P * 32, dtype=e.tdtype, device=e.device)
             ops.im2col_c3(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.cols)
         self.vout.ensure(n, e.tdtype, e.device)
@@ -251,6 +257,8 @@ class BlockStage(Stage):
             rows = ops.conv3x3_stat_rows(e.dt, n, self.vout.h, self.vout.w, self.cin, cout)
         elif self.kind == "t2":
             rows = ops.tconv_stat_rows(e.dt, n, self.vin.h, self.vin.w, self.cin, cout)
+        elif self.direct:
+            rows = ops.conv_c3_stat_rows(n, self.vout.h, self.vout.w)
         else:
             rows = ops.fwd_stat_rows(e.dt, m, ncols)
         stats = torch.empty(rows * 2 * ncols, device=e.device, dtype=torch.float32)
@@ -380,10 +388,13 @@ class BlockStage(Stage):
         targets = self._sum_targets() if self.fold_active else []
         fz = self._fused_target(n, targets)
         # with a fused producer BN the dgrad needs this weight gradient's sums first
-        ctx = contextlib.nullcontext() if fz else e.side(dz, psum, getattr(self, "cols", None))
+        ctx = contextlib.nullcontext() if fz else e.side(dz, psum, getattr(self, "cols", None),
+                                                         e.x_in if self.direct else None)
         with ctx:
             raw = torch.empty_like(dw) if targets else None
-            if self.kind == "c3in":
+            if self.kind == "c3in" and self.direct:
+                ops.conv_c3_wgrad(e.x_in, n, e.h_valid, self.vout.h, self.vout.w, dz, dw)
+            elif self.kind == "c3in":
                 ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
                                dw, dw_cols=27)
             elif self.kind == "c3":

@@ -124,6 +124,23 @@ def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0, fold=None, raw=None)
          stream_ptr())
 
 
+def conv_c3_stat_rows(n, h, w):
+    return query("cnnitmo_conv_c3_stat_rows", n, h, w)
+
+
+def conv_c3_fwd(x, n, h_valid, h, w, wt, bias, out: View, flags=0, aff=None, stats=None):
+    """First layer, bf16, patches built in LDS from the fp32 input (no im2col buffer)."""
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_conv_c3_fwd", ptr(x), n, h_valid, h, w, ptr(wt), ptr(bias), out.ptr, out.ld, out.off, flags,
+         ptr(sc), ptr(sh), ptr(stats), stream_ptr())
+
+
+def conv_c3_wgrad(x, n, h_valid, h, w, dz, dw):
+    ws = workspace(query("cnnitmo_conv_c3_wgrad_workspace_bytes", n, h, w), dz.device)
+    call("cnnitmo_conv_c3_wgrad", ptr(x), n, h_valid, h, w, ptr(dz), ptr(dw), ws.data_ptr(), ws.numel(),
+         stream_ptr())
+
+
 def im2col_c3(dt, x, n, h_valid, h, w, cols):
     call("cnnitmo_im2col_c3", dt, ptr(x), n, h_valid, h, w, ptr(cols), stream_ptr())
 

@@ -149,6 +149,21 @@ int cnnitmo_conv1tap_fwd(int dtype, const void* cols, int k, long m, const void*
                          int flags, const float* aff_scale, const float* aff_shift,
                          float* stat_part, void* stream);
 
+/* First layer without im2col (bf16): x [n,h_valid,w,3] fp32 -> out view [n,h,w,32]
+ * (ld, off), rows >= h_valid of the input read as zero (pad-to-16).  wt: [32][32]
+ * bf16 packed columns (cnnitmo_prep_c3_weights); flags/aff as conv3x3_fwd;
+ * stat_part [rows][2][32] with rows = cnnitmo_conv_c3_stat_rows.  Replaces
+ * cnnitmo_im2col_c3 + cnnitmo_conv1tap_fwd for model.py:208. */
+long cnnitmo_conv_c3_stat_rows(int n, int h, int w);
+int cnnitmo_conv_c3_fwd(const float* x, int n, int h_valid, int h, int w, const void* wt,
+                        const float* bias, void* out, int out_ld, int out_off, int flags,
+                        const float* aff_scale, const float* aff_shift, float* stat_part, void* stream);
+/* dw [32][27] fp32 (OVERWRITTEN; OHWI) = sum_p dz[p][co] * patch(x, p)[k], dz [n*h*w][32]
+ * bf16 contiguous.  Replaces cnnitmo_conv_wgrad(ntaps = 1) over im2col columns. */
+size_t cnnitmo_conv_c3_wgrad_workspace_bytes(int n, int h, int w);
+int cnnitmo_conv_c3_wgrad(const float* x, int n, int h_valid, int h, int w, const void* dz, float* dw,
+                          void* workspace, size_t ws_bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Conv2DTranspose(f, 2, strides=2, 'valid') -- replaces model.py:200
  * (ConvBNTranspose).  x [n,h,w,cin] contiguous; k: [2][2][cout][cin] dtype;
