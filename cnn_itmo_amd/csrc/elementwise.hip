@@ -352,36 +352,52 @@ extern "C" int cnnitmo_bn_bwd_finalize(const float* part, long rows, int c, doub
 // NP = 1: partial sums of dz per channel (bias gradient); NP = 4: split by the
 // pixel's (h&1, w&1) parity, i.e. per Conv2DTranspose tap of the producer
 // (needed by the folded-BN wgrad correction of the tconv; db = their sum).
-template <typename T, int NP, bool ROUTE>
+// G3: dy is the rank-3 product dy[p][c] = sum_o g3[p][o] * wh[o][c] of the sigmoid
+// head's per-pixel output gradient g3 and its [3][C] weights (cnnitmo_head_fwd_bwd_g3),
+// formed in fp32 on the fly instead of being read as a C-channel tensor.
+template <typename T, int NP, bool ROUTE, bool G3 = false>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, long dy_ld, int dy_off,
                                     const T* __restrict__ r, long r_ld, int r_off, long P, int C,
                                     const float* __restrict__ coef, int nobn, int drop,
                                     uint64_t dbase, T* __restrict__ dz, float* __restrict__ part,
                                     int H, int W, const T* __restrict__ dyp,
-                                    const uint8_t* __restrict__ pidx) {
+                                    const uint8_t* __restrict__ pidx, const float* __restrict__ g3,
+                                    const float* __restrict__ wh) {
   constexpr int VE = Vec16<T>::N;
   const int tpp = C / VE, rows = 256 / tpp;
   const int tid = threadIdx.x;
   const int row = tid / tpp, cv = tid - row * tpp, c0 = cv * VE;
   float acc[NP][VE];
   float ca[VE], cb[VE], ce[VE];
+  float w3[G3 ? 3 : 1][VE];
 #pragma unroll
   for (int e = 0; e < VE; ++e) {
 #pragma unroll
     for (int k = 0; k < NP; ++k) acc[k][e] = 0.f;
+    if constexpr (G3) {
+#pragma unroll
+      for (int o = 0; o < 3; ++o) w3[o][e] = row < rows ? wh[o * C + c0 + e] : 0.f;
+    }
     const bool ok = row < rows && !nobn;
     ca[e] = ok ? coef[c0 + e] : 1.f;
     cb[e] = ok ? coef[C + c0 + e] : 0.f;
     ce[e] = ok ? coef[2 * C + c0 + e] : 0.f;
   }
   if (row < rows) {
+    const int hw = H * W;  // ROUTE / NP 4 index math in 32 bits (checked by the launchers)
     for (long p = (long)blockIdx.x * rows + row; p < P; p += (long)gridDim.x * rows) {
       float g[VE], rv[VE];
-      load_dy<T>(dy, dy_ld, dy_off, p, C, c0, drop, dbase, g);
+      if constexpr (G3) {
+        const float q0 = g3[p * 3], q1 = g3[p * 3 + 1], q2 = g3[p * 3 + 2];
+#pragma unroll
+        for (int e = 0; e < VE; ++e) g[e] = q0 * w3[0][e] + q1 * w3[1][e] + q2 * w3[2][e];
+      } else {
+        load_dy<T>(dy, dy_ld, dy_off, p, C, c0, drop, dbase, g);
+      }
       Pack16<T>::load(r + (size_t)p * r_ld + r_off + c0, rv);
       if constexpr (ROUTE) {  // + the MaxPooling2D gradient routed to this pixel
-        const long hw = (long)H * W;
-        const int n = (int)(p / hw), rem = (int)(p - n * hw);
+        const int pi = (int)p;
+        const int n = pi / hw, rem = pi - n * hw;
         const int hh = rem / W, ww = rem - hh * W, Ho = H / 2, Wo = W / 2;
         if ((hh >> 1) < Ho && (ww >> 1) < Wo) {
           const long po = ((long)n * Ho + (hh >> 1)) * Wo + (ww >> 1);
@@ -409,7 +425,7 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ dy, long dy_ld, int dy
       Pack16<T>::store(dz + (size_t)p * C + c0, g);
       int k = 0;
       if constexpr (NP == 4) {
-        const int rem = (int)(p % ((long)H * W));
+        const int rem = (int)p % hw;
         const int hh = rem / W, ww = rem - hh * W;
         k = ((hh & 1) << 1) | (ww & 1);
       }
@@ -440,10 +456,11 @@ extern "C" int cnnitmo_bn_bwd_apply(int dtype, const void* dy, int dy_ld, int dy
   CNN_REQUIRE(nobn || coef, "bn_bwd_apply: missing coefficients");
   const bool par = flags & CNNITMO_PARITY;
   CNN_REQUIRE(!par || (h > 0 && w > 0), "bn_bwd_apply: PARITY needs h, w");
+  CNN_REQUIRE(!par || p < (1L << 31), "bn_bwd_apply: too many pixels");
 #define BNA(T, NP)                                                                                \
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, NP, false>), dim3(G), dim3(256), 0, s, (const T*)dy, \
                      (long)dy_ld, dy_off, (const T*)r, (long)r_ld, r_off, p, c, coef, nobn, drop, \
-                     base, (T*)dz, part, h, w, nullptr, nullptr)
+                     base, (T*)dz, part, h, w, nullptr, nullptr, nullptr, nullptr)
   if (dtype == CNNITMO_BF16) {
     if (par) BNA(bf16, 4); else BNA(bf16, 1);
   } else {
@@ -463,15 +480,35 @@ extern "C" int cnnitmo_bn_bwd_apply_pooled(int dtype, const void* dy, int dy_ld,
   const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
   CNN_REQUIRE(c % 8 == 0 && c / VE <= 256 && dy_ld % 8 == 0 && dy_off % 8 == 0 && r_ld % 8 == 0 &&
               r_off % 8 == 0 && coef && dy_pool && idx, "bn_bwd_apply_pooled: unsupported arguments (c=%d)", c);
+  CNN_REQUIRE(p < (1L << 31), "bn_bwd_apply_pooled: too many pixels");
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, 1, true>), dim3(G), dim3(256), 0, s, (const bf16*)dy,
                        (long)dy_ld, dy_off, (const bf16*)r, (long)r_ld, r_off, p, c, coef, 0, 0, (uint64_t)0,
-                       (bf16*)dz, part, h, w, (const bf16*)dy_pool, idx);
+                       (bf16*)dz, part, h, w, (const bf16*)dy_pool, idx, nullptr, nullptr);
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<float, 1, true>), dim3(G), dim3(256), 0, s, (const float*)dy,
                        (long)dy_ld, dy_off, (const float*)r, (long)r_ld, r_off, p, c, coef, 0, 0, (uint64_t)0,
-                       (float*)dz, part, h, w, (const float*)dy_pool, idx);
+                       (float*)dz, part, h, w, (const float*)dy_pool, idx, nullptr, nullptr);
   return cnnitmo_check_launch("bn_bwd_apply_pooled");
+}
+
+extern "C" int cnnitmo_bn_bwd_apply_g3(int dtype, const float* g3, const float* wh, const void* r, int r_ld,
+                                       int r_off, long p, int c, const float* coef, void* dz, float* part,
+                                       void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int G = cnnitmo_bn_bwd_rows(p, c);
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % VE == 0 && c / VE <= 256 && r_ld % VE == 0 && r_off % VE == 0 && coef && g3 && wh,
+              "bn_bwd_apply_g3: unsupported arguments (c=%d)", c);
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, 1, false, true>), dim3(G), dim3(256), 0, s, nullptr, 0L, 0,
+                       (const bf16*)r, (long)r_ld, r_off, p, c, coef, 0, 0, (uint64_t)0, (bf16*)dz, part, 0, 0,
+                       nullptr, nullptr, g3, wh);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<float, 1, false, true>), dim3(G), dim3(256), 0, s, nullptr, 0L, 0,
+                       (const float*)r, (long)r_ld, r_off, p, c, coef, 0, 0, (uint64_t)0, (float*)dz, part, 0,
+                       0, nullptr, nullptr, g3, wh);
+  return cnnitmo_check_launch("bn_bwd_apply_g3");
 }
 
 // ----------------------------------------------------------------------------
@@ -487,10 +524,11 @@ __global__ void maxpool_fwd_kernel(const T* __restrict__ x, long x_ld, int x_off
   const long total = (long)N * Ho * Wo * cv;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
        i += (long)gridDim.x * blockDim.x) {
-    const long po = i / cv;
+    const int pi = (int)(i / cv);  // 32-bit index math from here (launcher: < 2^31 pixels)
+    const long po = pi;
     const int c0 = (int)(i - po * cv) * VE;
-    const int n = (int)(po / ((long)Ho * Wo));
-    const int rem = (int)(po - (long)n * Ho * Wo);
+    const int n = pi / (Ho * Wo);
+    const int rem = pi - n * (Ho * Wo);
     const int ho = rem / Wo, wo = rem - ho * Wo;
     float best[VE];
     uint8_t arg[VE];
@@ -534,8 +572,8 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
   const int Ho = H / 2, Wo = W / 2;
   if (row >= rows) return;
   for (long po = (long)blockIdx.x * rows + row; po < Pp; po += (long)gridDim.x * rows) {
-    const int n = (int)(po / ((long)Ho * Wo));
-    const int rem = (int)(po - (long)n * Ho * Wo);
+    const int n = (int)po / (Ho * Wo);  // 32-bit index math (launcher: < 2^31 pixels)
+    const int rem = (int)po - n * (Ho * Wo);
     const int ho = rem / Wo, wo = rem - ho * Wo;
     float g[VE];
     Pack16<T>::load(dy + (size_t)po * C + c0, g);
@@ -582,8 +620,8 @@ __global__ void pool_bnsums_kernel(const T* __restrict__ dyp, const uint8_t* __r
   }
   if (row < rows) {
     for (long po = (long)blockIdx.x * rows + row; po < Pp; po += (long)gridDim.x * rows) {
-      const int n = (int)(po / ((long)Ho * Wo));
-      const int rem = (int)(po - (long)n * Ho * Wo);
+      const int n = (int)po / (Ho * Wo);  // 32-bit index math (launcher: < 2^31 pixels)
+      const int rem = (int)po - n * (Ho * Wo);
       const int ho = rem / Wo, wo = rem - ho * Wo;
       float g[VE], rw[4][VE];
       Pack16<T>::load(dyp + (size_t)po * C + c0, g);
@@ -613,6 +651,7 @@ extern "C" int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_
   hipStream_t s = (hipStream_t)stream;
   CNN_REQUIRE(c % 8 == 0 && x_ld % 8 == 0 && x_off % 8 == 0, "maxpool_fwd: channels must be multiples of 8");
   const long work = (long)n * (h / 2) * (w / 2) * c;
+  CNN_REQUIRE((long)n * (h / 2) * (w / 2) < (1L << 31), "maxpool_fwd: too many pixels");
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(grid_for(work / 8)), dim3(256), 0, s,
                        (const bf16*)x, (long)x_ld, x_off, n, h, w, c, (bf16*)y, idx, scale, shift);
@@ -648,6 +687,7 @@ extern "C" int cnnitmo_pool_bnsums(int dtype, const void* dyp, const uint8_t* id
   CNN_REQUIRE(c % 8 == 0 && r_ld % 8 == 0 && r_off % 8 == 0 && c / VE <= 256,
               "pool_bnsums: unsupported channel count %d", c);
   const long Pp = (long)n * (h / 2) * (w / 2);
+  CNN_REQUIRE(Pp < (1L << 31), "pool_bnsums: too many pixels");
   const int G = cnnitmo_bn_bwd_rows(Pp, c);
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL(pool_bnsums_kernel<bf16>, dim3(G), dim3(256), 0, s, (const bf16*)dyp, idx, h, w, Pp, c,
@@ -673,7 +713,8 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
                             const float* __restrict__ wt, const float* __restrict__ bias,
                             const float* __restrict__ target, float* __restrict__ yhat,
                             T* __restrict__ dx, float inv_numel, float* __restrict__ part,
-                            const float* __restrict__ fs, const float* __restrict__ fh) {
+                            const float* __restrict__ fs, const float* __restrict__ fh,
+                            float* __restrict__ g3) {
   constexpr int VE = Vec16<T>::N;
   const int lpp = cin / VE;             // lanes per pixel (power of two <= 64)
   const int ppb = 256 / lpp;            // pixels per block iteration
@@ -700,6 +741,7 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
     for (int e = 0; e < VE; ++e) dwacc[o][e] = 0.f;
   float lsum = 0.f, corr = 0.f, db[3] = {0.f, 0.f, 0.f};
   const long P = (long)N * H * W;
+  const int hw = H * W;
   for (long base = (long)blockIdx.x * ppb; base < P; base += (long)gridDim.x * ppb) {
     const long p = base + slot;
     const bool inb = p < P;
@@ -721,8 +763,8 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
     float yh[3];
 #pragma unroll
     for (int o = 0; o < 3; ++o) yh[o] = 1.f / (1.f + expf(-z[o]));
-    const int n = inb ? (int)(p / ((long)H * W)) : 0;
-    const int rem = inb ? (int)(p - (long)n * H * W) : 0;
+    const int n = inb ? (int)p / hw : 0;  // 32-bit index math (P < 2^31, checked by the launchers)
+    const int rem = inb ? (int)p - n * hw : 0;
     const int h = rem / W, wc = rem - h * W;
     const bool valid = inb && h < Hv;
     const size_t tix = (((size_t)n * Hv + h) * W + wc) * 3;
@@ -751,15 +793,23 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
     if (sub == 0) {
       db[0] += dz[0]; db[1] += dz[1]; db[2] += dz[2];
     }
-    float g[VE];
 #pragma unroll
-    for (int e = 0; e < VE; ++e) {
-      g[e] = dz[0] * w[0][e] + dz[1] * w[1][e] + dz[2] * w[2][e];
+    for (int e = 0; e < VE; ++e)
 #pragma unroll
       for (int o = 0; o < 3; ++o) dwacc[o][e] += dz[o] * v[e];
+    if (g3) {  // rank-3 input gradient: the consumer forms dz . w itself
+      if (inb && sub == 0) {
+        g3[p * 3] = dz[0];
+        g3[p * 3 + 1] = dz[1];
+        g3[p * 3 + 2] = dz[2];
+      }
+    } else {
+      float g[VE];
+#pragma unroll
+      for (int e = 0; e < VE; ++e) g[e] = dz[0] * w[0][e] + dz[1] * w[1][e] + dz[2] * w[2][e];
+      if (inb) Pack16<T>::store(dx + (size_t)p * cin + c0, g);
     }
-    if (inb) Pack16<T>::store(dx + (size_t)p * cin + c0, g);
-  }
+    }
   if (!BWD) return;
   // reduce: lanes with equal `sub` hold the same channel slice
   __shared__ float red[256][3 * 8 + 5];
@@ -796,34 +846,50 @@ extern "C" int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_va
   CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
               "head: cin/%d must be a power of two <= 64", VE);
   const long P = (long)n * h * w;
+  CNN_REQUIRE(P < (1L << 31), "head: too many pixels");
   const int G = cnnitmo_head_rows(P);
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL((head_kernel<bf16, false>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
-                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale, shift);
+                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale, shift, nullptr);
   else
     hipLaunchKernelGGL((head_kernel<float, false>), dim3(G), dim3(256), 0, s, (const float*)x, n, h,
-                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale, shift);
+                       h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale, shift, nullptr);
   return cnnitmo_check_launch("head_fwd");
+}
+
+static int head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin, const float* wt,
+                        const float* b, const float* scale, const float* shift, const float* target, void* dx,
+                        float* g3, float* part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
+              "head: cin/%d must be a power of two <= 64", VE);
+  const long P = (long)n * h * w;
+  CNN_REQUIRE(P < (1L << 31), "head: too many pixels");
+  const int G = cnnitmo_head_rows(P);
+  const float inv_numel = (float)(1.0 / ((double)n * h_valid * w * 3));
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL((head_kernel<bf16, true>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
+                       h_valid, w, cin, wt, b, target, nullptr, (bf16*)dx, inv_numel, part, scale, shift, g3);
+  else
+    hipLaunchKernelGGL((head_kernel<float, true>), dim3(G), dim3(256), 0, s, (const float*)x, n, h,
+                       h_valid, w, cin, wt, b, target, nullptr, (float*)dx, inv_numel, part, scale, shift, g3);
+  return cnnitmo_check_launch("head_fwd_bwd");
 }
 
 extern "C" int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w,
                                     int cin, const float* wt, const float* b, const float* scale,
                                     const float* shift, const float* target, void* dx, float* part,
                                     void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
-  CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
-              "head: cin/%d must be a power of two <= 64", VE);
-  const long P = (long)n * h * w;
-  const int G = cnnitmo_head_rows(P);
-  const float inv_numel = (float)(1.0 / ((double)n * h_valid * w * 3));
-  if (dtype == CNNITMO_BF16)
-    hipLaunchKernelGGL((head_kernel<bf16, true>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
-                       h_valid, w, cin, wt, b, target, nullptr, (bf16*)dx, inv_numel, part, scale, shift);
-  else
-    hipLaunchKernelGGL((head_kernel<float, true>), dim3(G), dim3(256), 0, s, (const float*)x, n, h,
-                       h_valid, w, cin, wt, b, target, nullptr, (float*)dx, inv_numel, part, scale, shift);
-  return cnnitmo_check_launch("head_fwd_bwd");
+  CNN_REQUIRE(dx, "head_fwd_bwd: null dx");
+  return head_fwd_bwd(dtype, x, n, h, h_valid, w, cin, wt, b, scale, shift, target, dx, nullptr, part, stream);
+}
+
+extern "C" int cnnitmo_head_fwd_bwd_g3(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
+                                       const float* wt, const float* b, const float* scale, const float* shift,
+                                       const float* target, float* g3, float* part, void* stream) {
+  CNN_REQUIRE(g3, "head_fwd_bwd_g3: null g3");
+  return head_fwd_bwd(dtype, x, n, h, h_valid, w, cin, wt, b, scale, shift, target, nullptr, g3, part, stream);
 }
 
 // Folded input BN (x = r, y = r*s + h): dW[o][c] = s[c]*sum(dz*r) + h[c]*db[o].

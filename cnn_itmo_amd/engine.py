@@ -63,6 +63,7 @@ class Value:
         self.fuse_into = None  # the single conv3x3 consumer whose dgrad applies this BN's backward
         self.bn_contrib = []  # per-step partial-sum tensors [rows][2][c] from the consumers
         self.pool_route = None  # (pooled gradient, argmax idx): a deferred MaxPooling2D backward
+        self.grad_g3 = None  # (g3 [p][3], head weights [3][c]): the gradient as the head's rank-3 factor
         self.cs = None  # coefficient buffers of the owner (persist across steps)
         self.ch = None
 
@@ -116,6 +117,7 @@ class Value:
         self.ginit = False
         self.bn_contrib = []
         self.pool_route = None
+        self.grad_g3 = None
 
 
 class Stage:
@@ -314,7 +316,8 @@ class BlockStage(Stage):
         cout = self.cout
         if not self.vout.ginit:
             raise RuntimeError(f"{self.name}: output gradient not initialised")
-        dy = self.vout.gview(n)
+        g3 = self.vout.grad_g3
+        dy = self.vout.gview(n) if g3 is None else None
         rows = ops.bn_bwd_rows(P, cout)
         dz = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
         part2 = torch.empty(rows * (4 if par else 1) * cout, device=e.device, dtype=torch.float32)
@@ -339,7 +342,11 @@ class BlockStage(Stage):
             coef = torch.empty(3 * cout, device=e.device, dtype=torch.float32)
             ops.bn_bwd_finalize(part, prow, cout, P, e.p(bn.name + "/gamma"), self.smean, self.sinv,
                                 e.g(bn.name + "/gamma"), e.g(bn.name + "/beta"), coef)
-            if v.pool_route is not None:
+            if g3 is not None:  # dy = g3 . W_head, formed inside the apply
+                assert not flags and v.pool_route is None, "rank-3 head gradient with dropout/parity/pool"
+                ops.bn_bwd_apply_g3(e.dt, g3[0], g3[1], self.r, cout, P, coef, dz, part2)
+                v.grad_g3 = None
+            elif v.pool_route is not None:
                 assert not flags, "pool routing with dropout/parity"
                 ops.bn_bwd_apply_pooled(e.dt, dy, self.r, cout, coef, v.pool_route[0], v.pool_route[1], dz,
                                         part2)
@@ -525,15 +532,33 @@ class HeadStage(Stage):
         ops.head_fwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
                      e.p(self.name + "/bias"), yhat)
 
+    def _rank3(self):
+        """The producer's BN backward can take the head's input gradient as its rank-3
+        factor g3 (dy = g3 . W): a folded BN output (sums from the head's raw sums),
+        no Dropout, consumed by the head alone.  CNNITMO_HEAD_G3=0: store dy."""
+        v, e = self.vin, self.eng
+        prod = v.producer
+        return (e.training and v.folded and v.sum_consumers == 1 and not v.place and prod is not None
+                and prod.bn is not None and prod.drop is None and prod.kind == "c3"
+                and os.environ.get("CNNITMO_HEAD_G3", "1") != "0")
+
     def loss_and_grad(self, n, target, loss_acc):
         e = self.eng
-        self.vin.ensure_grad(n, e.tdtype, e.device)
-        rows = ops.head_rows(n * self.vin.h * self.vin.w)
+        P = n * self.vin.h * self.vin.w
+        rows = ops.head_rows(P)
         part = torch.empty(rows * (5 + 3 * self.cin), device=e.device, dtype=torch.float32)
-        dx = self.vin.gview(n)
         aff = self.vin.coef() if e.training and self.vin.folded else None
-        ops.head_fwd_bwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
-                         e.p(self.name + "/bias"), target, dx.buf, part, aff)
+        wt = e.p(self.name + "/kernel")
+        if self._rank3():
+            g3 = torch.empty(P * 3, device=e.device, dtype=torch.float32)
+            ops.head_fwd_bwd_g3(e.dt, self.vin.view(n), e.h_valid, wt, e.p(self.name + "/bias"), target, g3,
+                                part, aff)
+            self.vin.grad_g3 = (g3, wt)
+        else:
+            self.vin.ensure_grad(n, e.tdtype, e.device)
+            dx = self.vin.gview(n)
+            ops.head_fwd_bwd(e.dt, self.vin.view(n), e.h_valid, wt, e.p(self.name + "/bias"), target, dx.buf,
+                             part, aff)
         v = self.vin
         raw = torch.empty(3 * self.cin, device=e.device, dtype=torch.float32) \
             if e.training and v.sum_consumers and v.folded else None

@@ -286,6 +286,19 @@ def head_fwd_bwd(dt, x: View, h_valid, wt, b, target, dx, part, aff=None):
          ptr(sh), ptr(target), ptr(dx), ptr(part), stream_ptr())
 
 
+def head_fwd_bwd_g3(dt, x: View, h_valid, wt, b, target, g3, part, aff=None):
+    """head_fwd_bwd whose input gradient leaves as g3 [p][3] (dx = g3 . W)."""
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_head_fwd_bwd_g3", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b), ptr(sc),
+         ptr(sh), ptr(target), ptr(g3), ptr(part), stream_ptr())
+
+
+def bn_bwd_apply_g3(dt, g3, wh, r, c, p, coef, dz, part):
+    rp, rld, roff = _rview(r, c)
+    call("cnnitmo_bn_bwd_apply_g3", dt, ptr(g3), ptr(wh), rp, rld, roff, p, c, ptr(coef), ptr(dz), ptr(part),
+         stream_ptr())
+
+
 def head_rows(p):
     return query("cnnitmo_head_rows", p)
 

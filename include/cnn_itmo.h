@@ -292,6 +292,12 @@ int cnnitmo_bn_bwd_apply_pooled(int dtype, const void* dy, int dy_ld, int dy_off
                                 int r_ld, int r_off, int n, int h, int w, int c, const float* coef,
                                 const void* dy_pool, const uint8_t* idx, void* dz, float* part,
                                 void* stream);
+/* The same for the BN output consumed by the sigmoid head: dy is never stored;
+ * dy[p][c] = sum_o g3[p][o] * wh[o][c] is formed in fp32 from the head's per-pixel
+ * output gradient g3 [p][3] (cnnitmo_head_fwd_bwd_g3) and its weights wh [3][c]
+ * (12 B per pixel read instead of 2*c). */
+int cnnitmo_bn_bwd_apply_g3(int dtype, const float* g3, const float* wh, const void* r, int r_ld, int r_off,
+                            long p, int c, const float* coef, void* dz, float* part, void* stream);
 /* BN-backward sums WITHOUT a pass over dy: for a BN output whose gradient is the
  * input-gradient of a linear consumer (mode 1 conv3x3, 2 tconv2x2, 3 the 1x1
  * head), part[2][c] = {sum dy, sum dy*rhat} over the consumer's input channels
@@ -328,6 +334,11 @@ int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, in
                          const float* wt, const float* b, const float* scale,
                          const float* shift, const float* target, void* dx, float* part,
                          void* stream);
+/* As cnnitmo_head_fwd_bwd, but the input gradient leaves as its rank-3 factor
+ * g3 [p][3] fp32 = dL/dz of the head (dx = g3 * W; see cnnitmo_bn_bwd_apply_g3). */
+int cnnitmo_head_fwd_bwd_g3(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
+                            const float* wt, const float* b, const float* scale, const float* shift,
+                            const float* target, float* g3, float* part, void* stream);
 int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
                           const float* scale, const float* shift, float* loss_acc, float* dw,
                           float* db, float* raw_out, void* workspace, void* stream);
