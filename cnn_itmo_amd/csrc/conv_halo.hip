@@ -34,6 +34,16 @@
 #ifndef HALO_EXP
 #define HALO_EXP 0
 #endif
+// 1: EPI 0 epilogue straight from the MFMA registers (operands swapped so a lane
+// holds 4 consecutive channels of one pixel: 8-byte buffer stores, DPP row sums,
+// no C tile in LDS, no barrier unless BN statistics are gathered); 0 (default):
+// LDS-staged.  Measured A/B (tools/ab_layers.sh, tools/ab_bench.sh): per layer
+// within +-5 % either way without statistics, and the training forward (with
+// statistics) 8 % slower (845 vs 917 TF/s): the epilogue's cost is the MFMA pipe
+// idling while all eight waves store, which neither variant hides.
+#ifndef HALO_REGEPI
+#define HALO_REGEPI 0
+#endif
 
 namespace {
 
@@ -78,6 +88,24 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
 #undef W1
     default: wait_vm<0>(); break;
   }
+}
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+// buffer resource over [p, p + 2 GB) from a wave-uniform pointer
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t out_rsrc(const void* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uintptr_t u = (uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a) |
+                      ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32)) << 32);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, (short)0, 0x7FFFFFF0, 0x00020000);
+}
+// sum over the 16 lanes of each DPP row (quad_perm xor 1, xor 2, then the half-row
+// and row mirrors): 4 VALU ops, no LDS crossbar traffic
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
 }
 
 __device__ __forceinline__ int hswz(int row, int piece) {
@@ -135,6 +163,7 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
   constexpr int NPI = C::NPI, NBI = C::NBI;
   constexpr int CPR = BN / 8;  // 16-byte output pieces per pixel
   constexpr int CPRP = CPR <= 4 ? 4 : (CPR <= 8 ? 8 : 16);  // EPI 1: lanes per pixel (power of 2)
+  constexpr bool REG = EPI == 0 && HALO_REGEPI && HALO_EXP == 0;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -278,6 +307,7 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           if constexpr (HALO_EXP == 2) acc[i][j][0] += __builtin_bit_cast(float, af[cur][i].x ^ bfr[cur][j].y);
+          else if constexpr (REG) Mma<bf16>::run(acc[i][j], bfr[cur][j], af[cur][i]);  // C^T: lanes = pixels
           else Mma<bf16>::run(acc[i][j], af[cur][i], bfr[cur][j]);
       // the next item's LDS-DMA pieces due after this tap
       if (pf) {
@@ -377,6 +407,93 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
         if (p.N < 0) *dst = v;
       } else {
         *dst = v;
+      }
+    }
+    zero_acc();
+  };
+
+  // REG: the epilogue straight from the (swapped-operand) accumulators: lane = pixel
+  // (lane & 15) of fragment f, 4 consecutive columns (lane >> 4) * 4 + r of
+  // fragment j.  Bias, border correction, ReLU, inference affine, then one 8-byte
+  // buffer store per (f, j) (out-of-image pixels: offset beyond the range, dropped;
+  // every lane issues FM*FN stores).  BN sums: DPP row sums over the 16 pixels of
+  // each fragment, then across the waves of each 256-pixel group through LDS.
+  auto epilogue_reg = [&](const Pos& e, int buf) {
+    const int img = e.img, y0 = e.y0, x0 = e.x0;
+    const int n0 = e.nb * BN;
+    const int oh0 = y0 + wave * RPW;
+    const bf16* base = MODE == 0
+                           ? (const bf16*)p.out + (((size_t)img * p.ho + oh0) * p.wo + x0) * p.out_ld + p.out_off
+                           : (const bf16*)p.out + (((size_t)img * 2 * p.ho + 2 * oh0) * 2 * p.wo + 2 * x0) * p.out_ld +
+                                 p.out_off;
+    const __amdgpu_buffer_rsrc_t os = out_rsrc(base);
+    float s1[FN][4], s2[FN][4];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = j * 16 + (lane >> 4) * 4;  // first of this lane's 4 columns in the block
+      const int n = n0 + c;
+      const int tp = MODE == 1 ? n / p.cout : 0, co = MODE == 1 ? n - tp * p.cout : n;
+      // 16-byte loads: 4 | column, parameter slices 16-byte aligned
+      const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + ((p.flags & CNNITMO_BIAS_PER_COL) ? n : co))
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 s4 = aff ? *reinterpret_cast<const float4*>(p.aff_scale + co) : make_float4(1.f, 1.f, 1.f, 1.f);
+      const float4 h4 = aff ? *reinterpret_cast<const float4*>(p.aff_shift + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float bj[4] = {b4.x, b4.y, b4.z, b4.w}, sj[4] = {s4.x, s4.y, s4.z, s4.w}, hj[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int rr = f / FMR, col = (f % FMR) * 16 + (lane & 15);
+        const int oh = oh0 + rr, ow = x0 + col;
+        const bool ok = oh < p.ho && ow < p.wo;
+        bf16 o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[f][j][r] + bj[r];
+          if (p.border) v -= border_corr(p.border + (size_t)(n + r) * 8, oh, ow, p.ho, p.wo);
+          if (relu) v = fmaxf(v, 0.f);
+          if (aff) v = v * sj[r] + hj[r];
+          const float vs = ok ? v : 0.f;
+          s1[j][r] += vs;
+          s2[j][r] += vs * vs;
+          o[r] = from_f32<bf16>(v);
+        }
+        u32x2 pk;
+        __builtin_memcpy(&pk, o, 8);
+        const long el = MODE == 0 ? ((long)rr * p.wo + col) * p.out_ld + co
+                                  : ((long)(2 * rr + (tp >> 1)) * 2 * p.wo + 2 * col + (tp & 1)) * p.out_ld + co;
+        __builtin_amdgcn_raw_buffer_store_b64(pk, os, ok ? (unsigned)(el * 2) : 0x80000000u, 0, 0);
+      }
+    }
+    if (stats) {
+      // every wave has left the stage before the sums reuse it
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem + buf * STAGE);  // [NWAVE][BN][2]
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a1 = row16_sum(s1[j][r]), a2 = row16_sum(s2[j][r]);
+          if ((lane & 15) == 0) {
+            const int c = j * 16 + (lane >> 4) * 4 + r;
+            red[(wave * BN + c) * 2 + 0] = a1;
+            red[(wave * BN + c) * 2 + 1] = a2;
+          }
+        }
+      __syncthreads();
+      if (tid < C::SG * BN) {
+        const int g = tid / BN, col = tid - g * BN;
+        constexpr int WPG = NWAVE / C::SG;  // waves per 256-pixel group
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPG; ++w) {
+          t1 += red[((g * WPG + w) * BN + col) * 2 + 0];
+          t2 += red[((g * WPG + w) * BN + col) * 2 + 1];
+        }
+        const long tile = ((long)img * h.tiles_y + y0 / TH) * h.tiles_x + x0 / TW;
+        float* st = p.stats + (size_t)(tile * C::SG + g) * 2 * p.N;
+        st[n0 + col] = t1;
+        st[p.N + n0 + col] = t2;
       }
     }
     zero_acc();
@@ -528,7 +645,7 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
   // count is a lower bound for waves whose stats stores were exec-masked off,
   // which only makes their wait stricter.
   // output store instructions per wave
-  constexpr int NST = EPI ? RPW * TW * CPRP / 64 : (RPW * TW * CPR + 63) / 64;
+  constexpr int NST = EPI ? RPW * TW * CPRP / 64 : (REG ? FM * FN : (RPW * TW * CPR + 63) / 64);
   static_assert(RPW * TW * CPR % 64 == 0, "every lane issues the same number of stores");
   // BN partial sums are stored by threads tid < SG*BN: waves 0 .. (SG*BN-1)/64
   // EPI 1: the sums stores are not counted (an undercount only makes a wait stricter)
@@ -564,7 +681,8 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
       mq[ST - 1] = issued;
     }
     if (ep.ch == nch - 1) {
-      if constexpr (HALO_EXP != 7) __syncthreads();  // every wave is done reading this stage: reuse it for the C tile
+      // every wave is done reading this stage: reuse it for the C tile (REG: no C tile)
+      if constexpr (HALO_EXP != 7 && !REG) __syncthreads();
       if constexpr (HALO_EXP == 3) {
         if (p.N < 0) {  // never: keeps the MFMA results alive
           float t = 0.f;
@@ -577,6 +695,7 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
         zero_acc();
       } else {
         if constexpr (EPI == 1) epilogue_bnb(ep, buf);
+        else if constexpr (REG) epilogue_reg(ep, buf);
         else epilogue(ep, buf);
         issued += S;
       }
