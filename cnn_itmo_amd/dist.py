@@ -26,6 +26,11 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (several ranks on one GPU): CNNITMO_DIST_BACKEND=gloo and
+    # CNNITMO_DEVICE=<index> (every rank on that device)
+    if os.environ.get("CNNITMO_DEVICE") is not None:
+        local = int(os.environ["CNNITMO_DEVICE"])
+    backend = backend or os.environ.get("CNNITMO_DIST_BACKEND") or None
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
