@@ -338,6 +338,7 @@ extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int ci
 
 extern "C" long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int cin, int cout) {
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false)) return tconv_stream_rows(n, h, w);
+  if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout)) return tconv_ws_rows(cin, cout);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
   a.cin = cin; a.N = 4 * cout; a.a_ld = cin; a.out_ld = cout; a.M = (long)n * h * w;
@@ -400,6 +401,8 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
                                                     int dgrad) {
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(dgrad ? 1 : 0, h, w, cin, cout, false))
     return tconv_stream_name(dgrad ? 1 : 0, h, w, cin, cout, false);
+  if (dtype == CNNITMO_BF16 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout))
+    return tconv_ws_name(dgrad ? 1 : 0, cin, cout);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
   a.cin = dgrad ? cout : cin;
@@ -509,6 +512,9 @@ extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int 
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false))
     return launch_tconv_stream(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
                                aff_shift, stat_part, nullptr, nullptr, 0, 0, (hipStream_t)stream, "tconv2x2_fwd");
+  if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout))
+    return launch_tconv_ws(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
+                           aff_shift, stat_part, (hipStream_t)stream, "tconv2x2_fwd");
   return dispatch(dtype, a, stream, "tconv2x2_fwd");
 }
 
@@ -528,6 +534,9 @@ extern "C" int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h,
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(1, h, w, cin, cout, false))
     return launch_tconv_stream(1, dout, cout, 0, kT, n, h, w, cin, cout, dx, cin, 0, nullptr, 0, nullptr, nullptr,
                                nullptr, nullptr, nullptr, 0, 0, (hipStream_t)stream, "tconv2x2_dgrad");
+  if (dtype == CNNITMO_BF16 && tconv_ws_handles(1, cin, cout))
+    return launch_tconv_ws(1, dout, cout, 0, kT, n, h, w, cin, cout, dx, cin, 0, nullptr, 0, nullptr, nullptr,
+                           nullptr, (hipStream_t)stream, "tconv2x2_dgrad");
   return dispatch(dtype, a, stream, "tconv2x2_dgrad");
 }
 

@@ -1,0 +1,305 @@
+// Conv2DTranspose(2, strides=2) forward and input-gradient for up6..up8
+// (model.py:199-200, ConvBNTranspose) as WEIGHT-STATIONARY GEMMs whose waves
+// never synchronise after the prologue.
+//
+// A workgroup (8 waves, one per CU) owns one column block of the GEMM: its
+// weight block [BN][K] (<= 132 KB, rows padded by 16 B so the 16 rows of a B
+// fragment hit distinct banks) is copied into LDS once.  Then every wave walks
+// its own 32-pixel tiles: A fragments come straight from HBM/L2 into registers
+// (16-byte loads, two K-steps in flight), B fragments from LDS, the MFMA runs
+// with the operands swapped (C^T: a lane holds 4 consecutive columns of one
+// pixel) and the epilogue stores from registers.  No barrier after the
+// prologue: one wave's epilogue overlaps the other waves' MFMAs -- the bubble
+// that bounds the tile-synchronous kernels on these short-K GEMMs.
+//
+// The nblk column blocks of a pixel range run on the workgroups of one XCD, so
+// the A tile every block re-reads is an L2 hit (blockIdx % 8 = XCD).
+//
+// MODE 0 (forward): A = x [P][cin] view, B = k [4*cout][cin] (n = tap*cout + co),
+//   out pixel (2y + tap/2, 2x + tap%2); bias (per column or channel), ReLU,
+//   inference affine, BN partial sums: one row per wave (rows = tconv_ws_rows).
+// MODE 1 (input gradient): A row of input pixel (y, x) = the four dout pixels
+//   (2y+a, 2x+b) x cout (k = tap*cout + co), B = kT [cin][4*cout]; dx [P][cin].
+#include <cstdio>
+
+#include "igemm_common.h"
+
+namespace {
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+constexpr int NW = 8;  // waves per workgroup
+
+struct WSArgs {
+  const bf16* a;
+  long a_ld;
+  int a_off;
+  const bf16* b;  // [N][K]
+  int nimg, h, w, cout, K, N;
+  bf16* out;
+  long out_ld;
+  int out_off;
+  const float* bias;
+  int flags;
+  const float* aff_scale;
+  const float* aff_shift;
+  float* stats;  // [rows][2][N]
+  int nblk, gpx;  // column blocks; pixel groups per XCD
+  long tiles;     // 32-pixel tiles
+};
+
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+template <int MODE, int BN>
+__global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
+  constexpr int FN = BN / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int K = p.K, ldsrow = K * 2 + 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
+  const int nb = i % p.nblk, grp = i / p.nblk;
+  const int gidx = xcd * p.gpx + grp, ngrp = 8 * p.gpx;
+  const long per = (p.tiles + ngrp - 1) / ngrp;
+  const long t0 = gidx * per, t1 = t0 + per < p.tiles ? t0 + per : p.tiles;
+  // the weight block, once
+  const int pieces = K / 8;
+  for (int q = tid; q < BN * pieces; q += NW * 64) {
+    const int row = q / pieces, pc = q - row * pieces;
+    *reinterpret_cast<uint4*>(smem + row * ldsrow + pc * 16) =
+        *reinterpret_cast<const uint4*>(p.b + (size_t)(nb * BN + row) * K + pc * 8);
+  }
+  __syncthreads();
+
+  const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE, stats = p.flags & CNNITMO_STATS;
+  const int hw = p.h * p.w;
+  const long P = (long)p.nimg * hw;
+  const int frow = lane & 15, kq = lane >> 4;
+  // per-lane column constants (4 consecutive columns per fragment j)
+  float s1[MODE == 0 ? FN : 1][4], s2[MODE == 0 ? FN : 1][4];
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+  }
+  const char* Bl = smem + frow * ldsrow + kq * 16;
+  const int nks = K / 32;
+
+  for (long t = t0 + wave; t < t1; t += NW) {
+    // the lane's two pixels (fragment rows), clamped for the loads of a tail tile
+    long px[2];
+    const bf16* abase[2];
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      px[f] = t * 32 + f * 16 + frow;
+      const long pc = px[f] < P ? px[f] : P - 1;
+      if constexpr (MODE == 0) {
+        abase[f] = p.a + pc * p.a_ld + p.a_off + kq * 8;
+      } else {
+        const int pi = (int)pc, img = pi / hw, rem = pi - img * hw, y = rem / p.w, x = rem - y * p.w;
+        abase[f] = p.a + (((size_t)img * 2 * p.h + 2 * y) * 2 * p.w + 2 * x) * p.cout + kq * 8;
+      }
+    }
+    auto loadA = [&](int ks, uint4* dst) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        if constexpr (MODE == 0) {
+          dst[f] = *reinterpret_cast<const uint4*>(abase[f] + ks * 32);
+        } else {
+          const int k0 = ks * 32, tap = k0 / p.cout, co = k0 - tap * p.cout;
+          dst[f] = *reinterpret_cast<const uint4*>(abase[f] + ((tap >> 1) * 2 * p.w + (tap & 1)) * p.cout + co);
+        }
+      }
+    };
+    f32x4 acc[2][FN];
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto compute = [&](int ks, const uint4* a) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const uint4 bfr = *reinterpret_cast<const uint4*>(Bl + j * 16 * ldsrow + ks * 64);
+#pragma unroll
+        for (int f = 0; f < 2; ++f) Mma<bf16>::run(acc[f][j], bfr, a[f]);  // C^T: lanes = pixels
+      }
+    };
+    uint4 A0[2], A1[2], A2[2];
+    loadA(0, A0);
+    if (nks > 1) loadA(1, A1);
+    for (int ks = 0; ks < nks; ks += 3) {
+      if (ks + 2 < nks) loadA(ks + 2, A2);
+      compute(ks, A0);
+      if (ks + 1 < nks) {
+        if (ks + 3 < nks) loadA(ks + 3, A0);
+        compute(ks + 1, A1);
+      }
+      if (ks + 2 < nks) {
+        if (ks + 4 < nks) loadA(ks + 4, A1);
+        compute(ks + 2, A2);
+      }
+    }
+    // epilogue from registers
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = nb * BN + j * 16 + kq * 4;  // first of the lane's 4 columns
+      if constexpr (MODE == 0) {
+        const int tap = n / p.cout, co = n - tap * p.cout;
+        const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + ((p.flags & CNNITMO_BIAS_PER_COL) ? n : co))
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 sc4 = aff ? *reinterpret_cast<const float4*>(p.aff_scale + co) : make_float4(1.f, 1.f, 1.f, 1.f);
+        const float4 sh4 = aff ? *reinterpret_cast<const float4*>(p.aff_shift + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float bj[4] = {b4.x, b4.y, b4.z, b4.w}, sj[4] = {sc4.x, sc4.y, sc4.z, sc4.w},
+                    hj[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          const bool ok = px[f] < P;
+          bf16 o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[f][j][r] + bj[r];
+            if (relu) v = fmaxf(v, 0.f);
+            if (aff) v = v * sj[r] + hj[r];
+            const float vs = ok ? v : 0.f;
+            s1[j][r] += vs;
+            s2[j][r] += vs * vs;
+            o[r] = from_f32<bf16>(v);
+          }
+          if (ok) {
+            const int pi = (int)px[f], img = pi / hw, rem = pi - img * hw, y = rem / p.w, x = rem - y * p.w;
+            const size_t op = ((size_t)img * 2 * p.h + 2 * y + (tap >> 1)) * 2 * p.w + 2 * x + (tap & 1);
+            u32x2 pk;
+            __builtin_memcpy(&pk, o, 8);
+            *reinterpret_cast<u32x2*>(p.out + op * p.out_ld + p.out_off + co) = pk;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          if (px[f] < P) {
+            bf16 o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = from_f32<bf16>(acc[f][j][r]);
+            u32x2 pk;
+            __builtin_memcpy(&pk, o, 8);
+            *reinterpret_cast<u32x2*>(p.out + (size_t)px[f] * p.out_ld + p.out_off + n) = pk;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (MODE == 0) {
+    if (stats) {  // one row per wave: row = (group, wave), columns of this block
+      const long row = (long)gidx * NW + wave;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = nb * BN + j * 16 + kq * 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float a1 = row16_sum(s1[j][r]), a2 = row16_sum(s2[j][r]);
+          if (frow == 0) {
+            p.stats[(size_t)row * 2 * p.N + n + r] = a1;
+            p.stats[(size_t)row * 2 * p.N + p.N + n + r] = a2;
+          }
+        }
+      }
+    }
+  }
+}
+
+struct WSPlan {
+  int bn, nblk, gpx;
+};
+
+bool ws_plan(int mode, int cin, int cout, WSPlan& pl) {
+  static const int en = [] {
+    const char* e = getenv("CNNITMO_TCONV_WS");
+    return e ? atoi(e) : 1;
+  }();
+  if (!en || cout % 32 || cin % 32) return false;
+  const int K = mode == 0 ? cin : 4 * cout, N = mode == 0 ? 4 * cout : cin;
+  // forward: 64 (the BN-sum accumulators would spill at 128); gradient: up to 128
+  int bn = mode == 0 ? 64 : 128;
+  while (bn >= 64 && (long)bn * (K * 2 + 16) > 132 * 1024) bn /= 2;
+  if (bn < 64 || N % bn) return false;
+  const int nblk = N / bn;
+  if (nblk > 32 || 32 % nblk) return false;
+  // where it measured faster than the halo / implicit-GEMM paths (tools/ab_env.sh,
+  // b32 1080p): the gradient at BN 128 (up8: 2.48 -> 1.87 ms) and the forward at
+  // 32 column blocks (up6: 1.53 -> 1.44 ms).  Elsewhere (up7 fwd/dgrad, up8 fwd) the
+  // A fragments re-read from L2 per 4-8 MFMAs bound it (BN 64).
+  static const int force = [] {
+    const char* e = getenv("CNNITMO_TCONV_WS");
+    return e ? atoi(e) : 1;
+  }();
+  if (force != 2 && !(mode == 1 ? bn == 128 : nblk == 32)) return false;
+  pl.bn = bn;
+  pl.nblk = nblk;
+  pl.gpx = 32 / nblk;
+  return true;
+}
+
+}  // namespace
+
+bool tconv_ws_handles(int mode, int cin, int cout) {
+  WSPlan pl;
+  return ws_plan(mode, cin, cout, pl);
+}
+
+// BN partial-sum rows of the forward: one per (pixel group, wave)
+long tconv_ws_rows(int cin, int cout) {
+  WSPlan pl;
+  if (!ws_plan(0, cin, cout, pl)) return 0;
+  return 8L * pl.gpx * NW;
+}
+
+const char* tconv_ws_name(int mode, int cin, int cout) {
+  WSPlan pl;
+  if (!ws_plan(mode, cin, cout, pl)) return "";
+  static thread_local char buf[64];
+  snprintf(buf, sizeof(buf), "tconv_ws_kernel<%d,%d>", mode, pl.bn);
+  return buf;
+}
+
+int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b, int n, int h, int w, int cin,
+                    int cout, void* out, long out_ld, int out_off, const float* bias, int flags,
+                    const float* aff_scale, const float* aff_shift, float* stats, hipStream_t s, const char* what) {
+  WSPlan pl;
+  CNN_REQUIRE(ws_plan(mode, cin, cout, pl), "%s: no weight-stationary plan", what);
+  CNN_REQUIRE(a_ld % 8 == 0 && a_off % 8 == 0 && out_ld % 4 == 0 && out_off % 4 == 0, "%s: misaligned views", what);
+  CNN_REQUIRE((long)n * h * w < (1L << 31), "%s: too many pixels", what);
+  CNN_REQUIRE(!(flags & CNNITMO_STATS) || (stats && mode == 0), "%s: STATS without buffer", what);
+  WSArgs t;
+  t.a = (const bf16*)a; t.a_ld = a_ld; t.a_off = a_off; t.b = (const bf16*)b;
+  t.nimg = n; t.h = h; t.w = w; t.cout = cout;
+  t.K = mode == 0 ? cin : 4 * cout;
+  t.N = mode == 0 ? 4 * cout : cin;
+  t.out = (bf16*)out; t.out_ld = out_ld; t.out_off = out_off;
+  t.bias = bias; t.flags = flags; t.aff_scale = aff_scale; t.aff_shift = aff_shift; t.stats = stats;
+  t.nblk = pl.nblk; t.gpx = pl.gpx;
+  t.tiles = ((long)n * h * w + 31) / 32;
+  const int grid = 8 * pl.gpx * pl.nblk;  // 256: one workgroup per CU
+  const size_t lds = (size_t)pl.bn * (t.K * 2 + 16);
+  static bool attr = [] {  // dynamic LDS beyond 64 KB
+    hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    return true;
+  }();
+  (void)attr;
+  if (mode == 0) {
+    if (pl.bn == 128) hipLaunchKernelGGL((tconv_ws_kernel<0, 128>), dim3(grid), dim3(NW * 64), lds, s, t);
+    else hipLaunchKernelGGL((tconv_ws_kernel<0, 64>), dim3(grid), dim3(NW * 64), lds, s, t);
+  } else {
+    if (pl.bn == 128) hipLaunchKernelGGL((tconv_ws_kernel<1, 128>), dim3(grid), dim3(NW * 64), lds, s, t);
+    else hipLaunchKernelGGL((tconv_ws_kernel<1, 64>), dim3(grid), dim3(NW * 64), lds, s, t);
+  }
+  return cnnitmo_check_launch(what);
+}
