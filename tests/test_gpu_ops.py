@@ -135,7 +135,10 @@ def test_conv_affine_inference_epilogue(dt, H, W):
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("cin,cout,H,W", [(64, 32, 3, 5), (128, 64, 4, 4), (512, 256, 2, 3),
                                           # bf16: the streamed kernel (resident weights), partial 64-px tiles
-                                          (128, 64, 3, 70), (256, 128, 5, 33), (128, 32, 2, 130)])
+                                          (128, 64, 3, 70), (256, 128, 5, 33), (128, 32, 2, 130),
+                                          # bf16 weight-stationary kernel: fwd at 32 column blocks
+                                          # (512 -> 512), dgrad at BN 128 (256 <- 128); ragged tiles
+                                          (512, 512, 3, 7), (256, 128, 7, 9)])
 def test_tconv(dt, cin, cout, H, W):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(cin)
