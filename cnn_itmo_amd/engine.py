@@ -366,7 +366,9 @@ class BlockStage(Stage):
             return None
         for m, ci0 in targets:
             if m.fuse_into is self and m.sum_consumers == 1:
-                if self.kind == "c3":
+                if self.kind == "c3" and self._split_fused(ci0, m.c):
+                    rows = ops.conv3x3_dgrad_bn_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, m.c, 0, m.c)
+                elif self.kind == "c3":
                     rows = ops.conv3x3_dgrad_bn_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, self.cin, ci0,
                                                      ci0 + m.c)
                 elif ci0 == 0 and m.c == self.cin and m.producer.kind != "t2":  # (no parity sums here)
@@ -376,6 +378,14 @@ class BlockStage(Stage):
                 if rows > 0:
                     return m, ci0, rows
         return None
+
+    def _split_fused(self, ci0, c):
+        """dec9's input gradient (concat [skip 32 | up 64], model.py:261): two launches
+        -- the skip columns as a plain 32-column dgrad and the up columns as a 64-column
+        dgrad with the fused BN backward -- instead of one with 48-column blocks whose
+        epilogue straddles both (measured 15 ms).  CNNITMO_SPLIT_DGRAD=0: one launch."""
+        return (ci0 > 0 and ci0 + c == self.cin and self.cin % 64 != 0 and c % 64 == 0 and ci0 % 32 == 0
+                and os.environ.get("CNNITMO_SPLIT_DGRAD", "1") != "0")
 
     def _weight_and_input_grads(self, n, P, par, dz, part2, rows):
         e = self.eng
@@ -443,7 +453,12 @@ class BlockStage(Stage):
             pin = n * self.vin.h * self.vin.w
             dzp = torch.empty(pin * m.c, dtype=e.tdtype, device=e.device)
             pp = torch.empty(frows * (4 if ppar else 1) * m.c, device=e.device, dtype=torch.float32)
-            if self.kind == "c3":
+            if self.kind == "c3" and self._split_fused(ci0, m.c):
+                h, w = self.vout.h, self.vout.w
+                ops.conv3x3_dgrad(e.dt, dz, n, h, w, cout, self.w_bwd, ci0, ops.View(dx.buf, n, h, w, ci0, dx.ld, dx.off))
+                wsub = self.w_bwd[ci0 * 9 * cout:]  # flipped weights [cin][3][3][cout]: rows ci0..
+                ops.conv3x3_dgrad_bn(e.dt, dz, n, h, w, cout, wsub, m.c, None, 0, m.c, coef, prod.r, dzp, pp, ppar)
+            elif self.kind == "c3":
                 ops.conv3x3_dgrad_bn(e.dt, dz, n, self.vout.h, self.vout.w, cout, self.w_bwd, self.cin, dx, ci0,
                                      ci0 + m.c, coef, prod.r, dzp, pp, ppar)
             else:
