@@ -742,6 +742,7 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
   float lsum = 0.f, corr = 0.f, db[3] = {0.f, 0.f, 0.f};
   const long P = (long)N * H * W;
   const int hw = H * W;
+  const bool rowal = W % ppb == 0;
   for (long base = (long)blockIdx.x * ppb; base < P; base += (long)gridDim.x * ppb) {
     const long p = base + slot;
     const bool inb = p < P;
@@ -763,9 +764,20 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
     float yh[3];
 #pragma unroll
     for (int o = 0; o < 3; ++o) yh[o] = 1.f / (1.f + expf(-z[o]));
-    const int n = inb ? (int)p / hw : 0;  // 32-bit index math (P < 2^31, checked by the launchers)
-    const int rem = inb ? (int)p - n * hw : 0;
-    const int h = rem / W, wc = rem - h * W;
+    // 32-bit index math (P < 2^31, checked by the launchers); when a block's ppb pixels
+    // never straddle a row (W % ppb == 0) it is wave-uniform: one scalar division
+    int n, h, wc;
+    if (rowal) {
+      const int b = (int)base, nb = b / hw, rb = b - nb * hw, hb = rb / W;
+      n = nb;
+      h = hb;
+      wc = rb - hb * W + slot;
+    } else {
+      n = inb ? (int)p / hw : 0;
+      const int rem = inb ? (int)p - n * hw : 0;
+      h = rem / W;
+      wc = rem - h * W;
+    }
     const bool valid = inb && h < Hv;
     const size_t tix = (((size_t)n * Hv + h) * W + wc) * 3;
     if (!BWD) {

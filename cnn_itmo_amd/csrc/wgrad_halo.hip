@@ -301,7 +301,13 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
   pl.bm = cout % 64 == 0 ? 64 : (cout == 32 ? 32 : 0);
   pl.bn = cin % 96 == 0 ? 96 : (cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0));
   if (!pl.bm || !pl.bn) return false;
-  pl.tw = (pl.bm * pl.bn <= 32 * 64 && w % 128 == 0) ? 128 : 64;
+  // 128-column strips also when w % 128 != 0 (a partial last strip): enc2a at 960
+  // columns 1.12 -> 0.99 ms (tools/ab_env.sh); CNNITMO_WH_TW128=0 restores 64
+  static const int tw128 = [] {
+    const char* e = getenv("CNNITMO_WH_TW128");
+    return e ? atoi(e) : 1;
+  }();
+  pl.tw = (pl.bm * pl.bn <= 32 * 64 && (w % 128 == 0 || (tw128 && w % 64 == 0))) ? 128 : 64;
   pl.strips = (w + pl.tw - 1) / pl.tw;  // a partial last strip reads zero columns
   pl.cbm = cout / pl.bm;
   pl.cbn = cin / pl.bn;
