@@ -41,6 +41,12 @@
 // within +-5 % either way without statistics, and the training forward (with
 // statistics) 8 % slower (845 vs 917 TF/s): the epilogue's cost is the MFMA pipe
 // idling while all eight waves store, which neither variant hides.
+// taps over which the next item's LDS-DMA pieces are issued (0 = all KT taps).
+// 5 of 9 (tools/ab_libs.sh, b32 1080p): dec6-dec9 + enc2b/enc3b fwd+dgrad
+// 64.4 -> 63.7 ms (dec7/dec8 fwd -2..4 %, the last pieces land sooner)
+#ifndef HALO_PF_TAPS
+#define HALO_PF_TAPS 5
+#endif
 #ifndef HALO_REGEPI
 #define HALO_REGEPI 0
 #endif
@@ -281,6 +287,8 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
   // Fragments are double-buffered across taps: tap t+1's ds_reads are issued
   // before tap t's MFMAs (pinned by sched barriers), so a whole tap of MFMAs
   // covers their latency instead of the just-in-time reads the scheduler emits.
+  // the next item's LDS-DMA pieces are spread over the first PFT taps
+  constexpr int PFT = HALO_PF_TAPS > 0 && HALO_PF_TAPS < KT ? HALO_PF_TAPS : KT;
   auto compute = [&](int buf, bool pf) {
     const char* Ps = smem + buf * STAGE;
     const char* Bs = Ps + C::PATCH;
@@ -313,7 +321,7 @@ __global__ __launch_bounds__((HaloCfg<MODE, TH, TW, BN, ST, EPI>::NT)) void halo
       if (pf) {
 #pragma unroll
         for (int k = 0; k < L; ++k)
-          if ((k * KT) / L == tap) issue_piece(k);
+          if ((k * PFT) / L == tap) issue_piece(k);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
