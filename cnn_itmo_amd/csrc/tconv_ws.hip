@@ -17,7 +17,8 @@
 //
 // MODE 0 (forward): A = x [P][cin] view, B = k [4*cout][cin] (n = tap*cout + co),
 //   out pixel (2y + tap/2, 2x + tap%2); bias (per column or channel), ReLU,
-//   inference affine, BN partial sums: one row per wave (rows = tconv_ws_rows).
+//   inference affine, BN partial sums (per tile, DPP row sums added into the
+//   wave's LDS slice; one row per wave at the end: rows = tconv_ws_rows).
 // MODE 1 (input gradient): A row of input pixel (y, x) = the four dout pixels
 //   (2y+a, 2x+b) x cout (k = tap*cout + co), B = kT [cin][4*cout]; dx [P][cin].
 #include <cstdio>
@@ -80,13 +81,11 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   const int hw = p.h * p.w;
   const long P = (long)p.nimg * hw;
   const int frow = lane & 15, kq = lane >> 4;
-  // per-lane column constants (4 consecutive columns per fragment j)
-  float s1[MODE == 0 ? FN : 1][4], s2[MODE == 0 ? FN : 1][4];
+  // BN sums: per tile, DPP row sums over the 16 pixels of each fragment are added
+  // into this wave's own [BN][2] fp32 slice of LDS (after the weight block)
+  float* sl = reinterpret_cast<float*>(smem + BN * ldsrow) + wave * BN * 2;
   if constexpr (MODE == 0) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+    for (int q = lane; q < BN * 2; q += 64) sl[q] = 0.f;
   }
   const char* Bl = smem + frow * ldsrow + kq * 16;
   const int nks = K / 32;
@@ -146,6 +145,7 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
       }
     }
     // epilogue from registers
+    float s1[MODE == 0 ? FN : 1][4], s2[MODE == 0 ? FN : 1][4];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = nb * BN + j * 16 + kq * 4;  // first of the lane's 4 columns
@@ -157,6 +157,8 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
         const float4 sh4 = aff ? *reinterpret_cast<const float4*>(p.aff_shift + co) : make_float4(0.f, 0.f, 0.f, 0.f);
         const float bj[4] = {b4.x, b4.y, b4.z, b4.w}, sj[4] = {sc4.x, sc4.y, sc4.z, sc4.w},
                     hj[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const bool ok = px[f] < P;
@@ -193,21 +195,29 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
         }
       }
     }
+    if constexpr (MODE == 0) {
+      if (stats) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float a1 = row16_sum(s1[j][r]), a2 = row16_sum(s2[j][r]);
+            if (frow == 0) {
+              const int c = j * 16 + kq * 4 + r;
+              sl[c * 2] += a1;
+              sl[c * 2 + 1] += a2;
+            }
+          }
+      }
+    }
   }
   if constexpr (MODE == 0) {
     if (stats) {  // one row per wave: row = (group, wave), columns of this block
+      __syncthreads();
       const long row = (long)gidx * NW + wave;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = nb * BN + j * 16 + kq * 4;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float a1 = row16_sum(s1[j][r]), a2 = row16_sum(s2[j][r]);
-          if (frow == 0) {
-            p.stats[(size_t)row * 2 * p.N + n + r] = a1;
-            p.stats[(size_t)row * 2 * p.N + p.N + n + r] = a2;
-          }
-        }
+      for (int q = lane; q < BN; q += 64) {
+        p.stats[(size_t)row * 2 * p.N + nb * BN + q] = sl[q * 2];
+        p.stats[(size_t)row * 2 * p.N + p.N + nb * BN + q] = sl[q * 2 + 1];
       }
     }
   }
@@ -224,21 +234,20 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl) {
   }();
   if (!en || cout % 32 || cin % 32) return false;
   const int K = mode == 0 ? cin : 4 * cout, N = mode == 0 ? 4 * cout : cin;
-  // forward: 64 (the BN-sum accumulators would spill at 128); gradient: up to 128
-  int bn = mode == 0 ? 64 : 128;
-  while (bn >= 64 && (long)bn * (K * 2 + 16) > 132 * 1024) bn /= 2;
+  int bn = 128;
+  while (bn >= 64 && (long)bn * (K * 2 + 16) + NW * bn * 8 > 148 * 1024) bn /= 2;
   if (bn < 64 || N % bn) return false;
   const int nblk = N / bn;
   if (nblk > 32 || 32 % nblk) return false;
   // where it measured faster than the halo / implicit-GEMM paths (tools/ab_env.sh,
-  // b32 1080p): the gradient at BN 128 (up8: 2.48 -> 1.87 ms) and the forward at
-  // 32 column blocks (up6: 1.53 -> 1.44 ms).  Elsewhere (up7 fwd/dgrad, up8 fwd) the
-  // A fragments re-read from L2 per 4-8 MFMAs bound it (BN 64).
+  // b32 1080p): every forward at BN 128 (up6 1.50 -> 1.08, up7 2.62 -> 1.98, up8
+  // 3.16 -> 2.98 ms) and the gradient at BN 128 (up8: 2.48 -> 1.87 ms); at BN 64
+  // (up7 gradient, K = 1024) the A fragments re-read from L2 per 4 MFMAs bound it.
   static const int force = [] {
     const char* e = getenv("CNNITMO_TCONV_WS");
     return e ? atoi(e) : 1;
   }();
-  if (force != 2 && !(mode == 1 ? bn == 128 : nblk == 32)) return false;
+  if (force != 2 && bn != 128) return false;
   pl.bn = bn;
   pl.nblk = nblk;
   pl.gpx = 32 / nblk;
@@ -285,7 +294,7 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
   t.nblk = pl.nblk; t.gpx = pl.gpx;
   t.tiles = ((long)n * h * w + 31) / 32;
   const int grid = 8 * pl.gpx * pl.nblk;  // 256: one workgroup per CU
-  const size_t lds = (size_t)pl.bn * (t.K * 2 + 16);
+  const size_t lds = (size_t)pl.bn * (t.K * 2 + 16) + (size_t)NW * pl.bn * 2 * sizeof(float);
   static bool attr = [] {  // dynamic LDS beyond 64 KB
     hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
