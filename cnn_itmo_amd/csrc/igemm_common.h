@@ -131,6 +131,11 @@ struct W2Label {
 W2Label wgrad2_label(long P, int M, int N, int ntaps);
 size_t wgrad2_ws_bytes(long P, int M, int N, int ntaps);
 
+// row-streaming bf16 tconv2x2 weight gradient (all four taps per block), wgrad_tconv.hip
+size_t wgrad_tconv_ws_bytes(int n, int h, int w, int cin, int cout);
+const char* wgrad_tconv_name(int n, int h, int w, int cin, int cout);
+int launch_wgrad_tconv(const bf16* x, long x_ld, int x_off, const bf16* dy, int n, int h, int w, int cin,
+                       int cout, float* ws, size_t ws_bytes, hipStream_t s);
 // sliding-window bf16 3x3 weight gradient for the high-resolution layers, wgrad_halo.hip
 size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout);
 const char* wgrad_halo_name(int n, int h, int w, int cin, int cout);

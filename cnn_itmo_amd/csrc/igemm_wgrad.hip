@@ -453,7 +453,7 @@ extern "C" size_t cnnitmo_wgrad_workspace_bytes(int dtype, int n, int h, int w, 
 extern "C" size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin,
                                                          int cout) {
   const long P = (long)n * h * w;
-  return dtype == CNNITMO_BF16 ? ws_bytes_for<bf16>(P, cout, cin, 4)
+  return dtype == CNNITMO_BF16 ? std::max(ws_bytes_for<bf16>(P, cout, cin, 4), wgrad_tconv_ws_bytes(n, h, w, cin, cout))
                                : ws_bytes_for<float>(P, cout, cin, 4);
 }
 
@@ -532,6 +532,19 @@ extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout
   a.M = cout; a.N = cin;
   a.tap_stride = (long)cout * cin; a.out_ld = cin;
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == CNNITMO_BF16) {
+    const int splits = launch_wgrad_tconv((const bf16*)x, cin, 0, (const bf16*)dout, n, h, w, cin, cout,
+                                          (float*)workspace, ws_bytes, s);
+    if (splits > 0) {
+      int rc = cnnitmo_check_launch("tconv2x2_wgrad");
+      if (rc) return rc;
+      const long slab = 4L * cout * cin;
+      const int rblocks = (int)std::min<long>((slab + 255) / 256, 4096);
+      hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)workspace, slab,
+                         splits, 4 * cout, cin, cin, dk, f);
+      return cnnitmo_check_launch("tconv2x2_wgrad");
+    }
+  }
   if (dtype == CNNITMO_BF16)
     return run_wgrad<bf16>(a, dk, 4 * cout, cin, cin, workspace, ws_bytes, s, "tconv2x2_wgrad", f, 1);
   if (dtype == CNNITMO_F32)
@@ -548,6 +561,10 @@ extern "C" const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, in
   if (dtype == CNNITMO_BF16 && ntaps == 9) {
     const char* hn = wgrad_halo_name(n, h, w, cin, cout);
     if (hn[0]) return hn;
+  }
+  if (dtype == CNNITMO_BF16 && ntaps == 4) {
+    const char* tn = wgrad_tconv_name(n, h, w, cin, cout);
+    if (tn[0]) return tn;
   }
   const long P = (long)n * h * w;
   static thread_local char buf[80];

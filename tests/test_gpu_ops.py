@@ -138,7 +138,9 @@ def test_conv_affine_inference_epilogue(dt, H, W):
                                           (128, 64, 3, 70), (256, 128, 5, 33), (128, 32, 2, 130),
                                           # bf16 weight-stationary kernel: fwd at 32 column blocks
                                           # (512 -> 512), dgrad at BN 128 (256 <- 128); ragged tiles
-                                          (512, 512, 3, 7), (256, 128, 7, 9)])
+                                          (512, 512, 3, 7), (256, 128, 7, 9),
+                                          # bf16 row-streaming wgrad: 4 rows per workgroup, 2 strips
+                                          (512, 512, 16, 40)])
 def test_tconv(dt, cin, cout, H, W):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(cin)

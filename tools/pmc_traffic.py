@@ -36,13 +36,16 @@ def unmangle(n):
 
 
 def label(name):
-    n = unmangle(name.replace(" ", ""))
+    n = unmangle(name.replace(" ", "")).replace("(anonymousnamespace)::", "")
     m = re.search(r"halo_gemm_kernel<(\d+),(\d+),(\d+),(\d+),\d+(?:,(\d+))?>", n)
     if m:
         return "halo_gemm_kernel<%s,%s,%s,%s%s>" % (m.groups()[:4] + (",bnb" if m.group(5) not in (None, "0") else "",))
     m = re.search(r"tconv_stream_kernel<(\d+),(\d+),\d+,(true|false)>", n)
     if m:
         return "tconv_stream_kernel<%s,%s%s>" % (m.group(1), m.group(2), ",bnb" if m.group(3) == "true" else "")
+    m = re.search(r"tconv_ws_kernel<(\d+),(\d+)>", n)
+    if m:
+        return "tconv_ws_kernel<%s,%s>" % m.groups()
     m = re.search(r"wgrad_halo_kernel<(\d+),(\d+),(\d+),", n)
     if m:
         return "wgrad_halo_kernel<%s,%s,%s>" % m.groups()
