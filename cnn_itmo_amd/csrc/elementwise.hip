@@ -704,6 +704,9 @@ extern "C" int cnnitmo_pool_bnsums(int dtype, const void* dyp, const uint8_t* id
 // part row layout: [loss, correct, db0..2, dW[3][cin]]
 // ----------------------------------------------------------------------------
 static constexpr int HEAD_BLOCKS = 1024;
+#ifndef HEAD_U
+#define HEAD_U 4
+#endif
 extern "C" int cnnitmo_head_rows(long p) {
   return (int)std::max<long>(1, std::min<long>(HEAD_BLOCKS, (p + 31) / 32));
 }
@@ -743,85 +746,100 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
   const long P = (long)N * H * W;
   const int hw = H * W;
   const bool rowal = W % ppb == 0;
-  for (long base = (long)blockIdx.x * ppb; base < P; base += (long)gridDim.x * ppb) {
-    const long p = base + slot;
-    const bool inb = p < P;
-    float v[VE];
-    if (inb) Pack16<T>::load(x + (size_t)p * cin + c0, v);
-    else
+  // HEAD_U pixel slots per lane group per iteration, all their loads issued first:
+  // one 16-byte load in flight per lane left this HBM pass at ~2 TB/s
+  for (long base0 = (long)blockIdx.x * ppb * HEAD_U; base0 < P; base0 += (long)gridDim.x * ppb * HEAD_U) {
+    float v[HEAD_U][VE], tg[HEAD_U][3];
+    bool inb[HEAD_U], valid[HEAD_U];
+    size_t tix[HEAD_U];
 #pragma unroll
-      for (int e = 0; e < VE; ++e) v[e] = 0.f;
-    float z[3];
+    for (int u = 0; u < HEAD_U; ++u) {
+      const long base = base0 + (long)u * ppb, p = base + slot;
+      inb[u] = p < P;
+      if (inb[u]) Pack16<T>::load(x + (size_t)p * cin + c0, v[u]);
+      else
 #pragma unroll
-    for (int o = 0; o < 3; ++o) {
-      float s = 0.f;
-#pragma unroll
-      for (int e = 0; e < VE; ++e) s += v[e] * wf[o][e];
-      for (int off = lpp >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      z[o] = s;
-    }
-    z[0] += b0; z[1] += b1; z[2] += b2;
-    float yh[3];
-#pragma unroll
-    for (int o = 0; o < 3; ++o) yh[o] = 1.f / (1.f + expf(-z[o]));
-    // 32-bit index math (P < 2^31, checked by the launchers); when a block's ppb pixels
-    // never straddle a row (W % ppb == 0) it is wave-uniform: one scalar division
-    int n, h, wc;
-    if (rowal) {
-      const int b = (int)base, nb = b / hw, rb = b - nb * hw, hb = rb / W;
-      n = nb;
-      h = hb;
-      wc = rb - hb * W + slot;
-    } else {
-      n = inb ? (int)p / hw : 0;
-      const int rem = inb ? (int)p - n * hw : 0;
-      h = rem / W;
-      wc = rem - h * W;
-    }
-    const bool valid = inb && h < Hv;
-    const size_t tix = (((size_t)n * Hv + h) * W + wc) * 3;
-    if (!BWD) {
-      if (valid && sub == 0) {
-        yhat[tix + 0] = yh[0];
-        yhat[tix + 1] = yh[1];
-        yhat[tix + 2] = yh[2];
+        for (int e = 0; e < VE; ++e) v[u][e] = 0.f;
+      // 32-bit index math (P < 2^31, checked by the launchers); when a block's ppb pixels
+      // never straddle a row (W % ppb == 0) it is wave-uniform: one scalar division
+      int n, h, wc;
+      if (rowal) {
+        const int b = (int)base, nb = b / hw, rb = b - nb * hw, hb = rb / W;
+        n = nb;
+        h = hb;
+        wc = rb - hb * W + slot;
+      } else {
+        n = inb[u] ? (int)p / hw : 0;
+        const int rem = inb[u] ? (int)p - n * hw : 0;
+        h = rem / W;
+        wc = rem - h * W;
       }
-      continue;
+      valid[u] = inb[u] && h < Hv;
+      tix[u] = (((size_t)n * Hv + h) * W + wc) * 3;
+      if (BWD) {
+#pragma unroll
+        for (int o = 0; o < 3; ++o) tg[u][o] = valid[u] ? target[tix[u] + o] : 0.f;
+      }
     }
-    float dz[3] = {0.f, 0.f, 0.f};
-    if (valid) {
-      const float t0 = target[tix], t1 = target[tix + 1], t2 = target[tix + 2];
-      const float e0 = yh[0] - t0, e1 = yh[1] - t1, e2 = yh[2] - t2;
+#pragma unroll
+    for (int u = 0; u < HEAD_U; ++u) {
+      const long p = base0 + (long)u * ppb + slot;
+      float z[3];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) {
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < VE; ++e) s += v[u][e] * wf[o][e];
+        for (int off = lpp >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        z[o] = s;
+      }
+      z[0] += b0; z[1] += b1; z[2] += b2;
+      float yh[3];
+#pragma unroll
+      for (int o = 0; o < 3; ++o) yh[o] = 1.f / (1.f + expf(-z[o]));
+      if (!BWD) {
+        if (valid[u] && sub == 0) {
+          yhat[tix[u] + 0] = yh[0];
+          yhat[tix[u] + 1] = yh[1];
+          yhat[tix[u] + 2] = yh[2];
+        }
+        continue;
+      }
+      float dz[3] = {0.f, 0.f, 0.f};
+      if (valid[u]) {
+        const float t0 = tg[u][0], t1 = tg[u][1], t2 = tg[u][2];
+        const float e0 = yh[0] - t0, e1 = yh[1] - t1, e2 = yh[2] - t2;
+        if (sub == 0) {
+          lsum += e0 * e0 + e1 * e1 + e2 * e2;
+          const int at = (t1 > t0) ? ((t2 > t1) ? 2 : 1) : ((t2 > t0) ? 2 : 0);
+          const int ap = (yh[1] > yh[0]) ? ((yh[2] > yh[1]) ? 2 : 1) : ((yh[2] > yh[0]) ? 2 : 0);
+          corr += (at == ap) ? 1.f : 0.f;
+        }
+        dz[0] = 2.f * e0 * yh[0] * (1.f - yh[0]) * inv_numel;
+        dz[1] = 2.f * e1 * yh[1] * (1.f - yh[1]) * inv_numel;
+        dz[2] = 2.f * e2 * yh[2] * (1.f - yh[2]) * inv_numel;
+      }
       if (sub == 0) {
-        lsum += e0 * e0 + e1 * e1 + e2 * e2;
-        const int at = (t1 > t0) ? ((t2 > t1) ? 2 : 1) : ((t2 > t0) ? 2 : 0);
-        const int ap = (yh[1] > yh[0]) ? ((yh[2] > yh[1]) ? 2 : 1) : ((yh[2] > yh[0]) ? 2 : 0);
-        corr += (at == ap) ? 1.f : 0.f;
+        db[0] += dz[0]; db[1] += dz[1]; db[2] += dz[2];
       }
-      dz[0] = 2.f * e0 * yh[0] * (1.f - yh[0]) * inv_numel;
-      dz[1] = 2.f * e1 * yh[1] * (1.f - yh[1]) * inv_numel;
-      dz[2] = 2.f * e2 * yh[2] * (1.f - yh[2]) * inv_numel;
-    }
-    if (sub == 0) {
-      db[0] += dz[0]; db[1] += dz[1]; db[2] += dz[2];
-    }
 #pragma unroll
-    for (int e = 0; e < VE; ++e)
+      for (int e = 0; e < VE; ++e)
 #pragma unroll
-      for (int o = 0; o < 3; ++o) dwacc[o][e] += dz[o] * v[e];
-    if (g3) {  // rank-3 input gradient: the consumer forms dz . w itself
-      if (inb && sub == 0) {
-        g3[p * 3] = dz[0];
-        g3[p * 3 + 1] = dz[1];
-        g3[p * 3 + 2] = dz[2];
+        for (int o = 0; o < 3; ++o) dwacc[o][e] += dz[o] * v[u][e];
+      if (g3) {  // rank-3 input gradient: the consumer forms dz . w itself
+        if (inb[u] && sub == 0) {
+          g3[p * 3] = dz[0];
+          g3[p * 3 + 1] = dz[1];
+          g3[p * 3 + 2] = dz[2];
+        }
+      } else {
+        float g[VE];
+#pragma unroll
+        for (int e = 0; e < VE; ++e) g[e] = dz[0] * w[0][e] + dz[1] * w[1][e] + dz[2] * w[2][e];
+        if (inb[u]) Pack16<T>::store(dx + (size_t)p * cin + c0, g);
       }
-    } else {
-      float g[VE];
-#pragma unroll
-      for (int e = 0; e < VE; ++e) g[e] = dz[0] * w[0][e] + dz[1] * w[1][e] + dz[2] * w[2][e];
-      if (inb) Pack16<T>::store(dx + (size_t)p * cin + c0, g);
     }
-    }
+  }
   if (!BWD) return;
   // reduce: lanes with equal `sub` hold the same channel slice
   __shared__ float red[256][3 * 8 + 5];
