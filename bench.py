@@ -8,18 +8,24 @@ storage / fp32 accumulation, one step = forward + backward + RCCL gradient
 all-reduce (N>1) + RMSprop, synthetic data (uniform /255 inputs and targets),
 random-init weights of the reference architecture (model.py:204-281).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+  python bench.py [--gpus N] [--steps K] [--warmup W]     (N>1: spawns N ranks itself)
+  torchrun --nproc-per-node N bench.py --gpus N ...       (one rank per GPU, RCCL)
 
 Prints ONE JSON line on rank 0.  `value` = frames/s over all ranks (weak
-scaling: 32 frames per GPU per step).  `roofline` is for the dominant kernel,
-timed live with HIP events on the compute stream over the timed steps;
-`cpu_baseline` times this repo's numpy oracle (oracle/unet_ref.py) on the host.
+scaling: 32 frames per GPU per step), timed over K steps with no per-launch
+instrumentation.  `roofline` is for the dominant kernel: a second pass of
+min(K, 10) steps brackets every conv launch with HIP events on the stream it
+runs on (its ms/step is reported beside).  `allreduce_exposed` (N>1) is the time
+the compute stream waits for the RCCL buckets after backward.  `cpu_baseline`
+times this repo's numpy oracle (oracle/unet_ref.py) on the host (rank 0, N=1).
+`fp32_infer` is BASELINE configs[1] (1080p b8 fp32 inference) with its own
+roofline and CPU baseline.
 """
 from __future__ import annotations
 
 import argparse
 import contextlib
+import functools
 import io
 import json
 import os
@@ -49,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-scale", type=int, default=2, help="CPU sample = 1 frame at H/s x W/s")
     ap.add_argument("--bucket-mb", type=float, default=16.0)
+    ap.add_argument("--infer-batch", type=int, default=8,
+                    help="fp32 inference leg (configs[1]) frames per GPU; 0 = skip")
     return ap.parse_args()
 
 
@@ -62,6 +70,7 @@ class KernelTimer:
         self.ops, self.torch = ops, torch
         self.on = False
         self.rec = []  # (name, flops, ev0, ev1)
+        self._pool, self._next = [], 0
         self._wrap()
 
     @staticmethod
@@ -76,22 +85,30 @@ class KernelTimer:
     def _bracket(self, name, flops, fn, *a, **k):
         if not self.on:
             return fn(*a, **k)
-        e0 = self.torch.cuda.Event(enable_timing=True)
-        e1 = self.torch.cuda.Event(enable_timing=True)
+        i = self._next
+        if i == len(self._pool):  # events are created once and reused pass after pass
+            self._pool.append((self.torch.cuda.Event(enable_timing=True), self.torch.cuda.Event(enable_timing=True)))
+        e0, e1 = self._pool[i]
+        self._next += 1
         e0.record()
         r = fn(*a, **k)
         e1.record()
         self.rec.append((name, flops, e0, e1))
         return r
 
+    def reset(self):
+        self.rec = []
+        self._next = 0
+
     def _wrap(self):
         ops = self.ops
+        query = functools.lru_cache(maxsize=None)(ops.query)  # kernel names: one ctypes query per shape
         o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
                                            "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
                                            "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad")}
 
         def kname(dt, n, h, w, cin, cout, dgrad):
-            return ops.query("cnnitmo_conv3x3_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
+            return query("cnnitmo_conv3x3_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
 
         def conv3x3_fwd(dt, x, wt, bias, out, *a, **k):
             fl = 2.0 * x.p * out.c * 9 * x.c
@@ -105,17 +122,17 @@ class KernelTimer:
 
         def conv3x3_dgrad_bn(dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1, *a, **k):
             fl = 2.0 * n * h * w * cin * 9 * cout
-            name = ops.query("cnnitmo_conv3x3_dgrad_bn_kernel_name", dt, n, h, w, cout, cin, c0, c1).decode()
+            name = query("cnnitmo_conv3x3_dgrad_bn_kernel_name", dt, n, h, w, cout, cin, c0, c1).decode()
             return self._bracket(name, fl, o["conv3x3_dgrad_bn"], dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1,
                                  *a, **k)
 
         def tconv_dgrad_bn(dt, dout, n, h, w, cout, kT, cin, *a, **k):
             fl = 2.0 * n * h * w * cin * 4 * cout
-            name = ops.query("cnnitmo_tconv2x2_dgrad_bn_kernel_name", dt, n, h, w, cout, cin).decode()
+            name = query("cnnitmo_tconv2x2_dgrad_bn_kernel_name", dt, n, h, w, cout, cin).decode()
             return self._bracket(name, fl, o["tconv_dgrad_bn"], dt, dout, n, h, w, cout, kT, cin, *a, **k)
 
         def tname(dt, n, h, w, cin, cout, dgrad):
-            return ops.query("cnnitmo_tconv2x2_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
+            return query("cnnitmo_tconv2x2_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
 
         def tconv_fwd(dt, x, k_, bias, out, *a, **k):
             fl = 2.0 * x.p * 4 * out.c * x.c
@@ -140,7 +157,7 @@ class KernelTimer:
             return self._bracket("conv_c3_wgrad_kernel + fold", fl, o["conv_c3_wgrad"], x, n, hv, h, w, *a, **k)
 
         def wname(dt, ntaps, n, h, w, cin, cout):
-            k = ops.query("cnnitmo_wgrad_kernel_name", dt, ntaps, n, h, w, cin, cout).decode()
+            k = query("cnnitmo_wgrad_kernel_name", dt, ntaps, n, h, w, cin, cout).decode()
             return k + " + slab_reduce"
 
         def conv_wgrad(dt, ntaps, x, dz, cout, dw, *a, **k):
@@ -171,10 +188,33 @@ class KernelTimer:
 
 
 # ---------------------------------------------------------------- CPU baseline
-def cpu_baseline(args, P_init, H, W):
-    """Time the numpy oracle (fp32, OpenBLAS sgemm) on one training step of ONE
-    frame at (H/s, W/s); report 1080p-frame-equivalents per second (FLOPs scale
-    with pixel count)."""
+def _host_info():
+    """(affinity cores, BLAS threads, CPU model) of this process's host."""
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    try:
+        from threadpoolctl import threadpool_info
+        blas = max([d.get("num_threads", 1) for d in threadpool_info()
+                    if d.get("internal_api") in ("openblas", "mkl")] or [1])
+    except Exception:  # pragma: no cover
+        blas = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    model = "unknown"
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:  # pragma: no cover
+        pass
+    return cores, blas, model
+
+
+def cpu_baseline(args, P_init, H, W, train=True):
+    """Time the numpy oracle (fp32, OpenBLAS sgemm, all BLAS threads) on ONE frame at
+    (H/s, W/s): a training step (fwd+bwd) or an inference forward; report
+    1080p-frame-equivalents per second (FLOPs scale with pixel count)."""
     from oracle import unet_ref as R
     s = args.cpu_scale
     h, w = H // s, W // s
@@ -184,28 +224,76 @@ def cpu_baseline(args, P_init, H, W):
     t = (rng.integers(0, 256, size=(1, h, w, 3)) / 255.0).astype(np.float32)
     net = R.UNetRef(P_init, np.float32)
     t0 = time.perf_counter()
-    net.forward(x, training=True, seed=0)
-    net.backward(t)
+    net.forward(x, training=train, seed=0)
+    if train:
+        net.backward(t)
     dt = time.perf_counter() - t0
-    try:
-        from threadpoolctl import threadpool_info
-        threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("internal_api") in ("openblas", "mkl")] or [1])
-    except Exception:  # pragma: no cover
-        threads = int(os.environ.get("OMP_NUM_THREADS", "1"))
+    cores, blas, model = _host_info()
     frac = (h * w) / float(H * W)
-    return {"value": frac / dt, "unit": "1080p frames/s (fwd+bwd, fp32)", "cores": threads, "kind": "port",
-            "sample": f"oracle/unet_ref.py numpy fp32 train step (fwd+bwd) on 1 frame {w}x{h} "
+    what = "train step (fwd+bwd)" if train else "inference forward (BN moving stats)"
+    return {"value": frac / dt, "unit": "1080p frames/s (%s, fp32)" % ("fwd+bwd" if train else "fwd"),
+            "cores": blas, "kind": "port",
+            "sample": f"oracle/unet_ref.py numpy fp32 {what} on 1 frame {w}x{h} "
                       f"({frac:.4f} of a 1920x{H} frame, scaled by pixel count); {dt:.2f} s",
-            "seconds": dt}
+            "seconds": dt, "affinity_cores": cores, "blas_threads": blas, "cpu_model": model}
+
+
+# ---------------------------------------------------------------- launcher
+def _spawn_ranks(args):
+    """`python bench.py --gpus N` without a torchrun environment: start N rank
+    processes (fresh children, before this process touches the GPU) under
+    torch.distributed.run on 127.0.0.1, relay rank 0's JSON line, exit with their
+    status."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd[1:6])} ...", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ---------------------------------------------------------------- legs
+def _roofline(agg, steps, elapsed, peak):
+    dom = max(agg.items(), key=lambda kv: kv[1][2])
+    name, (cnt, fl, ms) = dom
+    achieved = fl / (ms * 1e-3) / 1e12
+    step_flops = sum(v[1] for v in agg.values()) / steps
+    traffic = None
+    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            tab = json.load(open(pmc))
+            traffic = tab.get(name.split(" + ")[0], {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
+            "algorithmic_flop_per_launch": fl / cnt,
+            "step_conv_tflops": round(step_flops / (elapsed / steps) / 1e12, 2),
+            "step_mfma_frac": round(step_flops / (elapsed / steps) / 1e12 / peak, 4)}, step_flops
+
+
+def _print_agg(agg, tag):
+    for k, (c, f, m) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+        print(f"[bench:{tag}] {k:55s} launches={c:5d} time={m:9.1f} ms  {f / (m * 1e-3) / 1e12:7.1f} TFLOP/s",
+              file=sys.stderr)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args))
     import torch
     from cnn_itmo_amd import dist as D
     rank, world, local = D.init_from_env()
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a dp{world} "
+                         f"number as dp{args.gpus}")
     torch.cuda.set_device(local)
     import cnn_itmo_amd as C
     from cnn_itmo_amd import ops
@@ -217,7 +305,14 @@ def main():
                         verbose=False)
     P_init = model.named_weights() if rank == 0 else None
     eng = model._engine()
-    bucketer = D.attach(eng, bucket_mb=args.bucket_mb) if world > 1 else None
+    dp = None
+    if world > 1:
+        model.distribute(bucket_mb=args.bucket_mb)  # the public DP path (Model.fit_generator uses it)
+        dp = model._dp
+        pg_world = torch.distributed.get_world_size()
+        if rank == 0:
+            print(f"[bench] process group: backend={torch.distributed.get_backend()} world_size={pg_world}, "
+                  f"{len(dp.buckets)} gradient buckets", file=sys.stderr)
     timer = KernelTimer(ops, torch)
 
     g = torch.Generator(device="cuda")
@@ -234,9 +329,9 @@ def main():
             eng.stages[-1].infer(B, yhat)
             eng._release()
             return None
-        kw = dict(seed=i * 1000 + rank, lr=opt.lr, rho=opt.rho, eps=opt.epsilon)
-        if bucketer is not None:
-            kw.update(sync=bucketer.finish, grad_scale=bucketer.grad_scale)
+        kw = dict(seed=i * world + rank, lr=opt.lr, rho=opt.rho, eps=opt.epsilon)
+        if dp is not None:
+            kw.update(sync=dp.finish, grad_scale=dp.grad_scale)
         return eng.train_step(x, t, **kw)
 
     def barrier():
@@ -244,64 +339,75 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
+    def timed(n, first):
+        barrier()
+        t0 = time.perf_counter()
+        out = [step(first + i) for i in range(n)]
+        barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        return el.item(), out
+
     for i in range(args.warmup):
         step(i)
-    barrier()
-    timer.on = True
-    t0 = time.perf_counter()
-    losses = []
-    for i in range(args.steps):
-        losses.append(step(args.warmup + i))
-    barrier()
-    elapsed = time.perf_counter() - t0
-    timer.on = False
-    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-    elapsed = el.item()
+    # pass 1: throughput (no per-launch instrumentation inside the timed region)
+    elapsed, losses = timed(args.steps, args.warmup)
     frames = B * world * args.steps
     fps = frames / elapsed
+    # pass 2: the same steps with every conv launch bracketed by HIP events (roofline),
+    # and the all-reduce wait left exposed on the compute stream after overlap
+    timer.reset()
+    timer.on = True
+    if dp is not None:
+        dp.timing = True
+    k2 = max(1, min(args.steps, 10))
+    elapsed2, _ = timed(k2, args.warmup + args.steps)
+    timer.on = False
+    exposed = None
+    if dp is not None:
+        dp.timing = False
+        tot, n = dp.exposed_ms()
+        exposed = {"ms_per_step": round(tot / max(n, 1), 3), "steps": n, "buckets": len(dp.buckets),
+                   "bucket_mb": args.bucket_mb, "backend": torch.distributed.get_backend(),
+                   "world_size": torch.distributed.get_world_size()}
 
     agg = timer.summary()
-    dom = max(agg.items(), key=lambda kv: kv[1][2])
-    name, (cnt, fl, ms) = dom
     peak = BF16_PEAK_TF if args.dtype == "bfloat16" else F32_PEAK_TF
-    achieved = fl / (ms * 1e-3) / 1e12
-    total_fl = sum(v[1] for v in agg.values())
-    total_ms = sum(v[2] for v in agg.values())
-    step_flops = total_fl / args.steps
+    roof, step_flops = _roofline(agg, k2, elapsed2, peak)
+    roof["timed_pass_ms_per_step"] = round(elapsed2 / k2 * 1e3, 2)
     if rank == 0:
-        for k, (c, f, m) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
-            print(f"[bench] {k:55s} launches={c:5d} time={m:9.1f} ms  {f / (m * 1e-3) / 1e12:7.1f} TFLOP/s",
-                  file=sys.stderr)
+        _print_agg(agg, args.mode)
         if losses and losses[-1] is not None:
             print(f"[bench] last loss/acc: {losses[-1].cpu().numpy().tolist()}", file=sys.stderr)
         print(f"[bench] peak mem {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
-              f"step {elapsed / args.steps * 1e3:.1f} ms, conv share {total_ms / (elapsed * 1e3):.2%}",
-              file=sys.stderr)
+              f"step {elapsed / args.steps * 1e3:.1f} ms (instrumented pass {elapsed2 / k2 * 1e3:.1f} ms)"
+              + (f", exposed all-reduce {exposed['ms_per_step']} ms/step" if exposed else ""), file=sys.stderr)
 
-    traffic = None
-    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            tab = json.load(open(pmc))
-            key = name.split(" + ")[0]  # wgrad ops: the main kernel (slab_reduce excluded)
-            traffic = tab.get(key, {}).get("bytes_per_launch")
-        except Exception:
-            traffic = None
-    roof = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic,
-            "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
-            "algorithmic_flop_per_launch": fl / cnt,
-            "step_conv_tflops": round(step_flops / (elapsed / args.steps) / 1e12, 2),
-            "step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / peak, 4)}
+    replicas = None
+    if world > 1:  # DP correctness: every rank must hold the same parameters and moving stats
+        import hashlib
+        torch.cuda.synchronize()
+        dig = hashlib.sha256(eng.params.cpu().numpy().tobytes() + eng.bufs.cpu().numpy().tobytes()).hexdigest()
+        allg = [None] * world
+        torch.distributed.all_gather_object(allg, dig)
+        replicas = {"identical": len(set(allg)) == 1, "digests": sorted({d[:16] for d in allg})}
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "train":
+    if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            cpu = cpu_baseline(args, P_init, H, W)
+            cpu = cpu_baseline(args, P_init, H, W, train=args.mode == "train")
         except Exception as e:  # report, never fail the bench on the CPU leg
             cpu = {"error": repr(e)}
+
+    # configs[1]: fp32 inference leg (b8 1080p, BN moving stats), same ranks, weak
+    infer = None
+    if args.mode == "train" and args.infer_batch > 0:
+        del eng, model, x, t, losses
+        timer.rec = []
+        C.clear_session()
+        torch.cuda.empty_cache()
+        infer = infer_leg(args, rank, world, timer, barrier, P_init, H, W)
 
     if rank == 0:
         res = "1080p" if (args.height, args.width) == (1080, 1920) else f"{args.width}x{args.height}"
@@ -316,9 +422,86 @@ def main():
                            "padded": [H, W], "parallelism": f"dp{world}",
                            "gflop_per_frame": round(step_flops / B / 1e9, 1)},
                 "roofline": roof, "cpu_baseline": cpu}
+        if exposed is not None:
+            line["allreduce_exposed"] = exposed
+        if replicas is not None:
+            line["replicas"] = replicas
+        if infer is not None:
+            line["fp32_infer"] = infer
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def infer_leg(args, rank, world, timer, barrier, P_init, H, W):
+    """BASELINE configs[1]: 1080p frames, batch 8 per GPU, fp32, forward-only inference
+    (predict.py:62 semantics: BN moving stats), through Model.predict's engine path with
+    inputs resident in HBM.  Its own roofline (dominant kernel, HIP events) and CPU
+    baseline (the oracle's fp32 forward)."""
+    import torch
+    import cnn_itmo_amd as C
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = C.U_net(input_size=(args.height, args.width, 3), pad=True, dtype="float32", seed=0, verbose=False)
+    # non-trivial moving statistics (seeded), as a trained checkpoint would hold
+    rng = np.random.default_rng(5)
+    named = {}
+    for k, v in m.named_weights().items():
+        if k.endswith("/moving_mean"):
+            named[k] = rng.uniform(0.0, 0.5, v.shape).astype(np.float32)
+        elif k.endswith("/moving_variance"):
+            named[k] = rng.uniform(0.5, 2.0, v.shape).astype(np.float32)
+    m.set_named_weights(named)
+    P = m.named_weights() if rank == 0 else None
+    eng = m._engine()
+    B = args.infer_batch
+    g = torch.Generator(device="cuda")
+    g.manual_seed(77 + 7919 * rank)
+    x = torch.randint(0, 256, (B, args.height, args.width, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+    yhat = torch.empty(B, args.height, args.width, 3, device="cuda", dtype=torch.float32)
+
+    def step():
+        eng.forward(x, training=False)
+        eng.stages[-1].infer(B, yhat)
+        eng._release()
+
+    def timed(n):
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        return el.item()
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    k = max(args.steps, 5)
+    elapsed = timed(k)
+    timer.reset()
+    timer.on = True
+    k2 = min(k, 10)
+    elapsed2 = timed(k2)
+    timer.on = False
+    agg = timer.summary()
+    roof, step_flops = _roofline(agg, k2, elapsed2, F32_PEAK_TF)
+    roof["timed_pass_ms_per_step"] = round(elapsed2 / k2 * 1e3, 2)
+    out = {"metric": "1080p SDR->HDR frames/sec (fwd, inference)", "value": round(B * world * k / elapsed, 3),
+           "unit": "frames/s", "dtype": "f32", "steps": k, "ms_per_step": round(elapsed / k * 1e3, 2),
+           "config": {"workload": f"U-Net inference forward, {args.width}x{args.height} frames padded to "
+                                  f"{W}x{H}, {B} frames/GPU (BASELINE configs[1])", "global_batch": B * world,
+                      "gflop_per_frame": round(step_flops / B / 1e9, 1)},
+           "roofline": roof, "cpu_baseline": None}
+    if rank == 0:
+        _print_agg(agg, "infer")
+        if world == 1 and not args.no_cpu:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args, P, H, W, train=False)
+            except Exception as e:
+                out["cpu_baseline"] = {"error": repr(e)}
+    del eng, m, x, yhat
+    return out
 
 
 if __name__ == "__main__":

@@ -155,24 +155,63 @@ class ImageDataGenerator:
     # ---- iterators -------------------------------------------------------------------
     def flow_from_directory(self, directory, target_size=(256, 256), color_mode="rgb", classes=None,
                             class_mode="categorical", batch_size=32, shuffle=True, seed=None,
-                            interpolation="nearest", output="cuda", workers=8, **kwargs):
+                            interpolation="nearest", output="cuda", workers=8, rank=None, world=None, **kwargs):
+        """``batch_size`` is per rank; ``rank``/``world`` default to the initialised
+        torch.distributed group (pass ``world=1`` for an unsharded stream)."""
         return DirectoryIterator(directory, self, target_size, color_mode, classes, class_mode, batch_size,
-                                 shuffle, seed, interpolation, output, workers)
+                                 shuffle, seed, interpolation, output, workers, rank, world)
 
-    def flow(self, x, y=None, batch_size=32, shuffle=True, seed=None, output="cuda"):
-        return ArrayIterator(x, y, self, batch_size, shuffle, seed, output)
+    def flow(self, x, y=None, batch_size=32, shuffle=True, seed=None, output="cuda", rank=None, world=None):
+        return ArrayIterator(x, y, self, batch_size, shuffle, seed, output, rank, world)
+
+
+def _shard(rank, world):
+    """(rank, world) for a generator: explicit values, else the initialised
+    torch.distributed group, else (0, 1)."""
+    if world is None:
+        try:
+            from .dist import rank_world
+            r, w = rank_world()
+        except ImportError:  # pragma: no cover
+            r, w = 0, 1
+        return (r if rank is None else int(rank)), w
+    world = int(world)
+    rank = 0 if rank is None else int(rank)
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} out of range for world {world}")
+    return rank, world
 
 
 class Iterator:
-    """keras_preprocessing Iterator: batch index stream + seeded permutation."""
+    """keras_preprocessing Iterator: batch index stream + seeded permutation.
 
-    def __init__(self, n, batch_size, shuffle, seed):
+    Rank sharding: with ``world`` > 1 every rank replays the
+    SAME stream for a global batch of ``batch_size * world`` frames -- the same
+    reseeding, permutation and per-frame random transforms -- and keeps its
+    contiguous share (``np.array_split`` of the global batch; a short last batch is
+    split as evenly as possible).  The union over ranks is therefore exactly the
+    single-process stream at the global batch size, and two generators with the same
+    seed stay paired on every rank (main.py:82-100's ``zip``)."""
+
+    def __init__(self, n, batch_size, shuffle, seed, rank=None, world=None):
+        self.rank, self.world = _shard(rank, world)
+        if self.world > 1 and seed is None:
+            raise ValueError("a rank-sharded generator needs a seed shared by all ranks")
+        if self.world > 1 and n < self.world:
+            raise ValueError(f"{n} samples cannot be sharded over {self.world} ranks")
         self.n, self.batch_size, self.shuffle, self.seed = n, batch_size, shuffle, seed
+        self.global_batch = batch_size * self.world
         self.batch_index = 0
         self.total_batches_seen = 0
         self.index_array = None
         self.rng = np.random.RandomState(seed)
         self._gen = self._flow_index()
+
+    def _local(self, m):
+        """[lo, hi) of this rank's share of a global batch of m frames."""
+        q, rem = divmod(m, self.world)
+        lo = self.rank * q + min(self.rank, rem)
+        return lo, lo + q + (1 if self.rank < rem else 0)
 
     def reset(self):
         self.batch_index = 0
@@ -189,16 +228,17 @@ class Iterator:
                 self.rng.seed(self.seed + self.total_batches_seen)
             if self.batch_index == 0:
                 self._set_index_array()
-            cur = (self.batch_index * self.batch_size) % self.n
-            if self.n > cur + self.batch_size:
+            bs = self.global_batch
+            cur = (self.batch_index * bs) % self.n
+            if self.n > cur + bs:
                 self.batch_index += 1
             else:
                 self.batch_index = 0
             self.total_batches_seen += 1
-            yield self.index_array[cur:cur + self.batch_size]
+            yield self.index_array[cur:cur + bs]
 
     def __len__(self):
-        return (self.n + self.batch_size - 1) // self.batch_size
+        return (self.n + self.global_batch - 1) // self.global_batch
 
     def __iter__(self):
         return self
@@ -239,7 +279,7 @@ def load_img(path, target_size=None, color_mode="rgb", interpolation="nearest"):
 
 class DirectoryIterator(Iterator):
     def __init__(self, directory, gen, target_size, color_mode, classes, class_mode, batch_size, shuffle,
-                 seed, interpolation, output, workers):
+                 seed, interpolation, output, workers, rank=None, world=None):
         if class_mode not in (None, "input", "sparse", "categorical", "binary"):
             raise ValueError(f"Invalid class_mode: {class_mode}")
         self.gen, self.target_size = gen, tuple(target_size)
@@ -250,13 +290,17 @@ class DirectoryIterator(Iterator):
         self.class_indices = dict(zip(self.class_names, range(self.num_classes)))
         self._pool = cf.ThreadPoolExecutor(max_workers=workers)
         print(f"Found {len(self.filenames)} images belonging to {self.num_classes} classes.")
-        super().__init__(len(self.filenames), batch_size, shuffle, seed)
+        super().__init__(len(self.filenames), batch_size, shuffle, seed, rank, world)
 
     def _batch(self, index_array):
+        # the random stream covers the whole (global) batch; this rank keeps its share
+        shape = tuple(self.target_size) + ((1,) if self.color_mode == "grayscale" else (3,))
+        params = [self.gen.get_random_transform(shape, self.rng) for _ in index_array]
+        lo, hi = self._local(len(index_array))
+        index_array, params = index_array[lo:hi], params[lo:hi]
         frames = list(self._pool.map(
             lambda j: load_img(self.filenames[j], self.target_size, self.color_mode, self.interpolation),
             index_array))
-        params = [self.gen.get_random_transform(f.shape, self.rng) for f in frames]
         x = self.gen.transform_batch(np.stack(frames), params)
         if self.output == "numpy":
             x = x.cpu().numpy()
@@ -275,19 +319,21 @@ class DirectoryIterator(Iterator):
 class ArrayIterator(Iterator):
     """keras NumpyArrayIterator (flow): frames already in memory (uint8 or float)."""
 
-    def __init__(self, x, y, gen, batch_size, shuffle, seed, output):
+    def __init__(self, x, y, gen, batch_size, shuffle, seed, output, rank=None, world=None):
         self.x = np.asarray(x)
         if self.x.ndim != 4:
             raise ValueError(f"Input data in `NumpyArrayIterator` should have rank 4. Got {self.x.shape}")
         self.y = None if y is None else np.asarray(y)
         self.gen, self.output = gen, output
-        super().__init__(self.x.shape[0], batch_size, shuffle, seed)
+        super().__init__(self.x.shape[0], batch_size, shuffle, seed, rank, world)
 
     def _batch(self, index_array):
+        params = [self.gen.get_random_transform(self.x.shape[1:], self.rng) for _ in index_array]
+        lo, hi = self._local(len(index_array))
+        index_array, params = index_array[lo:hi], params[lo:hi]
         frames = self.x[index_array]
         if frames.dtype != np.uint8:
             frames = frames.astype(np.float32)
-        params = [self.gen.get_random_transform(f.shape, self.rng) for f in frames]
         x = self.gen.transform_batch(frames, params)
         if self.output == "numpy":
             x = x.cpu().numpy()

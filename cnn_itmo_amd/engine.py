@@ -766,6 +766,7 @@ class Engine:
         self.weights_dirty = True
         self.step = 0
         self.grad_hook = None  # callable(lo, hi) after each stage's gradients are written
+        self.fwd_hook = None  # callable() after the training forward (moving stats final)
         self._side = None  # side stream for weight gradients (CNNITMO_SIDE_STREAM=0: off)
         self._side_on = os.environ.get("CNNITMO_SIDE_STREAM", "1") != "0"
         # consumer dgrads apply their producer's BN backward (CNNITMO_FUSE_BNB=0: separate pass)
@@ -877,6 +878,8 @@ class Engine:
         """One fwd+bwd+RMSprop step.  Returns a device tensor [loss, acc]."""
         self.drop_seed = self.step if seed is None else int(seed)
         n = self.forward(x, training=True)
+        if self.fwd_hook:
+            self.fwd_hook()
         loss_acc = torch.empty(2, device=self.device, dtype=torch.float32)
         head = self.stages[-1]
         head.loss_and_grad(n, target.contiguous().float(), loss_acc)

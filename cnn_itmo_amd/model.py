@@ -6,6 +6,14 @@ Covers the model API the reference uses:
 ``predict(X)`` (predict.py:62), ``fit_generator(...)`` (main.py:126-132),
 ``train_on_batch``, ``evaluate``, ``save`` / ``load_model`` (predict.py:24,
 main.py:124) plus ``get_weights``/``set_weights`` in Keras layouts.
+
+Data parallelism sits behind the same calls: under torchrun (one
+process per GPU, ``dist.init_from_env()``), ``fit_generator(...,
+distributed=True)`` -- or any training call after ``model.distribute()`` --
+shards the batch stream per rank (each rank's generator yields its own batch;
+``flow_from_directory`` shards itself), all-reduces the gradients with RCCL
+during backward and averages the BN moving statistics (``dist.py``).  Epoch
+logs are global (all ranks' batches, weighted by size); callbacks run on rank 0.
 """
 from __future__ import annotations
 
@@ -74,6 +82,8 @@ class Model:
         self._weights = {}  # internal-layout numpy weights (host copy, authoritative before engine)
         self.optimizer = None
         self.engine = None
+        self._dp = None          # dist.GradBucketer once distribute() was called
+        self._dp_args = None
         self.dtype = "float32"
         self.stop_training = False
         self._init_weights(kwargs.get("seed", 0))
@@ -152,10 +162,12 @@ class Model:
         if dtype != self.dtype and self.engine is not None:
             self._weights.update(self.engine.get_weights())
             acc = self.engine.accum.clone()
+            step = self.engine.step
             self.engine = None
             self.dtype = dtype
             self._engine()
             self.engine.accum.copy_(acc)
+            self.engine.step = step  # the default dropout seed continues (no repeated masks)
         self.dtype = dtype
 
     def _engine(self):
@@ -176,7 +188,42 @@ class Model:
                     self.engine.accum.copy_(torch.as_tensor(pending[0]))
                     self.engine.step = pending[1]
                 self._pending_accum = None
+            if self._dp_args is not None:  # re-wire DP into a rebuilt engine (dtype switch)
+                from . import dist as D
+                self._dp = D.attach(self.engine, *self._dp_args, broadcast=False)
         return self.engine
+
+    # ---- data parallelism ----------------------------------------------------------
+    def distribute(self, bucket_mb=16.0, group=None):
+        """Train this model data-parallel over the initialised torch.distributed group
+        (one process per GPU; backend ``nccl`` = RCCL).  Rank 0's weights, moving stats
+        and optimizer state are broadcast first (DDP semantics).  Returns self."""
+        import torch.distributed as tdist
+        if not (tdist.is_available() and tdist.is_initialized()):
+            raise RuntimeError("distribute() needs an initialised process group (cnn_itmo_amd.dist.init_from_env)")
+        if self._dp is None:
+            from . import dist as D
+            self._dp_args = (float(bucket_mb), group)
+            self._dp = D.attach(self._engine(), bucket_mb, group)
+        return self
+
+    @property
+    def world(self):
+        """(rank, world) this model trains over (0, 1) when not distributed."""
+        if self._dp is None:
+            return 0, 1
+        from . import dist as D
+        return D.rank_world(self._dp_args[1])
+
+    def _allreduce_sum(self, vals):
+        """Sum a small host vector over the DP ranks (identity when not distributed)."""
+        if self._dp is None or self._dp.world == 1:
+            return np.asarray(vals, np.float64)
+        import torch
+        import torch.distributed as tdist
+        t = torch.tensor(np.asarray(vals, np.float64), device=self.engine.grads.device)
+        tdist.all_reduce(t, group=self._dp_args[1])
+        return t.cpu().numpy()
 
     @property
     def input_shape(self):
@@ -208,10 +255,18 @@ class Model:
             raise RuntimeError("You must compile your model before using it.")
 
     def train_on_batch(self, x, y, sync=True):
+        """One step on this rank's batch.  Distributed: the gradient is the mean over
+        ranks and every rank applies the same update; the returned loss/acc are this
+        rank's."""
         self._check_compiled()
         eng = self._engine()
         o = self.optimizer
-        la = eng.train_step(self._to_dev(x), self._to_dev(y), lr=o.lr, rho=o.rho, eps=o.epsilon)
+        kw = {}
+        if self._dp is not None:
+            r, w = self.world
+            # per-rank dropout masks: seed = step*world + rank (one stream per replica)
+            kw = dict(sync=self._dp.finish, grad_scale=self._dp.grad_scale, seed=eng.step * w + r)
+        la = eng.train_step(self._to_dev(x), self._to_dev(y), lr=o.lr, rho=o.rho, eps=o.epsilon, **kw)
         return la.cpu().numpy().tolist() if sync else la
 
     def evaluate(self, x, y, batch_size=32, verbose=0):
@@ -225,55 +280,87 @@ class Model:
             n += len(xb)
         return (tot / n).tolist()
 
-    def fit(self, x, y, batch_size=32, epochs=1, verbose=1, callbacks=None, shuffle=True, **kw):
+    def fit(self, x, y, batch_size=32, epochs=1, verbose=1, callbacks=None, shuffle=True, distributed=None,
+            **kw):
+        """keras Model.fit.  The permutation is drawn from numpy's global RNG each epoch
+        (as Keras does).  Distributed, ``batch_size`` is the GLOBAL batch: every rank
+        walks rank 0's permutation and trains on its contiguous share of each batch."""
+        if distributed or (distributed is None and self._dp is None and _dist_world() > 1):
+            self.distribute()
+        r, w = self.world
+
+        def perm():
+            idx = np.random.permutation(len(x)) if shuffle else np.arange(len(x))
+            if w > 1:
+                import torch.distributed as tdist
+                box = [idx]
+                tdist.broadcast_object_list(box, src=0, group=self._dp_args[1])
+                idx = box[0]
+            return idx
+
         def gen():
-            rng = np.random.default_rng(0)
             while True:
-                idx = rng.permutation(len(x)) if shuffle else np.arange(len(x))
+                idx = perm()
                 for i in range(0, len(x), batch_size):
-                    j = idx[i:i + batch_size]
+                    j = np.array_split(idx[i:i + batch_size], w)[r]
                     yield x[j], y[j]
         steps = -(-len(x) // batch_size)
         return self.fit_generator(gen(), steps_per_epoch=steps, epochs=epochs, verbose=verbose,
                                   callbacks=callbacks)
 
     def fit_generator(self, generator, steps_per_epoch=None, epochs=1, verbose=1, callbacks=None,
-                      validation_data=None, validation_steps=None, initial_epoch=0, **kwargs):
-        """keras Model.fit_generator (main.py:126-132): generator yields (x, y) batches."""
+                      validation_data=None, validation_steps=None, initial_epoch=0, distributed=None,
+                      **kwargs):
+        """keras Model.fit_generator (main.py:126-132): generator yields (x, y) batches.
+
+        Epoch loss/acc are means over samples (per-step values weighted by batch size,
+        as Keras does).  ``distributed=True`` (or None with an initialised process group
+        of more than one rank) trains data-parallel: each rank consumes its own
+        generator, logs are averaged over all ranks' samples, callbacks run on rank 0
+        only and a ``stop_training`` raised there stops every rank."""
         self._check_compiled()
+        if distributed or (distributed is None and self._dp is None and _dist_world() > 1):
+            self.distribute()
+        rank, world = self.world
         from .callbacks import CallbackList
-        cbs = CallbackList(callbacks or [], self)
+        cbs = CallbackList((callbacks or []) if rank == 0 else [], self)
         hist = History()
         self.stop_training = False
         cbs.call("on_train_begin", {})
         for epoch in range(initial_epoch, epochs):
             cbs.call("on_epoch_begin", epoch, {})
-            tot, t0 = np.zeros(2), time.time()
+            t0 = time.time()
             pending = []
             for step in range(steps_per_epoch):
                 xb, yb = next(generator)
                 cbs.call("on_batch_begin", step, {"batch": step, "size": len(xb)})
                 la = self.train_on_batch(xb, yb, sync=False)
-                pending.append(la)
+                pending.append((la, len(xb)))
                 cbs.call("on_batch_end", step, {"batch": step, "size": len(xb)})
-            for la in pending:
-                tot += la.cpu().numpy()
-            logs = {"loss": tot[0] / steps_per_epoch, "acc": tot[1] / steps_per_epoch}
+            tot = np.zeros(3)
+            for la, nb in pending:
+                tot[:2] += la.cpu().numpy() * nb
+                tot[2] += nb
+            tot = self._allreduce_sum(tot)
+            logs = {"loss": tot[0] / tot[2], "acc": tot[1] / tot[2]}
             if validation_data is not None:
-                vt, vn = np.zeros(2), 0
+                vt = np.zeros(3)
                 vsteps = validation_steps or 1
                 for _ in range(vsteps):
                     xv, yv = next(validation_data) if hasattr(validation_data, "__next__") else validation_data
-                    vt += np.asarray(self.evaluate(xv, yv, batch_size=len(xv)))
-                    vn += 1
-                logs["val_loss"], logs["val_acc"] = vt[0] / vn, vt[1] / vn
-            if verbose:
+                    vt[:2] += np.asarray(self.evaluate(xv, yv, batch_size=len(xv))) * len(xv)
+                    vt[2] += len(xv)
+                vt = self._allreduce_sum(vt)
+                logs["val_loss"], logs["val_acc"] = vt[0] / vt[2], vt[1] / vt[2]
+            if verbose and rank == 0:
                 msg = " - ".join(f"{k}: {v:.4f}" for k, v in logs.items())
                 print(f"Epoch {epoch + 1}/{epochs} - {time.time() - t0:.1f}s - {msg}", file=sys.stderr)
             hist.epoch.append(epoch)
             for k, v in logs.items():
                 hist.history.setdefault(k, []).append(v)
             cbs.call("on_epoch_end", epoch, logs)
+            if world > 1:
+                self.stop_training = bool(self._allreduce_sum([float(self.stop_training)])[0])
             if self.stop_training:
                 break
         cbs.call("on_train_end", {})
@@ -373,6 +460,14 @@ class Model:
             return
         with np.load(path, allow_pickle=False) as z:
             self.set_named_weights({k[2:]: z[k] for k in z.files if k.startswith("w/")})
+
+
+def _dist_world():
+    try:
+        import torch.distributed as tdist
+        return tdist.get_world_size() if tdist.is_available() and tdist.is_initialized() else 1
+    except ImportError:  # pragma: no cover
+        return 1
 
 
 def load_model(path, compile=True):

@@ -157,3 +157,57 @@ def test_gpu_paired_generators_feed_fit_generator(tmp_path):
         m = C.U_net(input_size=(32, 32, 3), verbose=False)
     h = m.fit_generator(gen, steps_per_epoch=2, epochs=1, verbose=0)
     assert np.isfinite(h.history["loss"][0])
+
+
+@pytest.mark.parametrize("world,nfr,bs", [(2, 11, 2), (3, 7, 1), (4, 9, 2)])
+def test_rank_shards_union_is_global_stream(world, nfr, bs):
+    """8e / 8f row 3: each rank's stream (batch bs) is its contiguous share of the
+    single-process stream at batch bs*world -- same frames, same random transforms,
+    ragged last batches split as evenly as possible."""
+    rng = np.random.default_rng(1)
+    frames = rng.integers(0, 256, (nfr, 8, 8, 3), dtype=np.uint8)
+    nb = 7
+    g = D.ImageDataGenerator(**REF_ARGS)
+    cap = _Capture(g)
+    it = g.flow(frames, batch_size=bs * world, seed=5, world=1)
+    for _ in range(nb):
+        next(it)
+    shards = []
+    for r in range(world):
+        gr = D.ImageDataGenerator(**REF_ARGS)
+        cr = _Capture(gr)
+        itr = gr.flow(frames, batch_size=bs, seed=5, rank=r, world=world)
+        assert len(itr) == len(it)
+        for _ in range(nb):
+            next(itr)
+        shards.append(cr.seen)
+    for b in range(nb):
+        fr, params = cap.seen[b]
+        got_fr = np.concatenate([shards[r][b][0] for r in range(world)])
+        got_p = sum((shards[r][b][1] for r in range(world)), [])
+        np.testing.assert_array_equal(got_fr, fr)
+        assert got_p == params
+        sizes = [len(shards[r][b][0]) for r in range(world)]
+        assert max(sizes) - min(sizes) <= 1
+
+
+def test_rank_shards_stay_paired_and_validate():
+    """Two generators with the same seed zip into pairs on every rank (main.py:99)."""
+    rng = np.random.default_rng(2)
+    frames = rng.integers(0, 256, (6, 8, 8, 3), dtype=np.uint8)
+    for r in range(2):
+        ga, gb = D.ImageDataGenerator(**REF_ARGS), D.ImageDataGenerator(**REF_ARGS)
+        ca, cb = _Capture(ga), _Capture(gb)
+        ia = ga.flow(frames, batch_size=2, seed=1, rank=r, world=2)
+        ib = gb.flow(frames, batch_size=2, seed=1, rank=r, world=2)
+        for _ in range(4):
+            next(ia), next(ib)
+        for (fa, pa), (fb, pb) in zip(ca.seen, cb.seen):
+            np.testing.assert_array_equal(fa, fb)
+            assert pa == pb
+    with pytest.raises(ValueError):
+        D.ImageDataGenerator().flow(frames, batch_size=2, seed=None, rank=0, world=2)
+    with pytest.raises(ValueError):
+        D.ImageDataGenerator().flow(frames, batch_size=2, seed=1, rank=2, world=2)
+    with pytest.raises(ValueError):
+        D.ImageDataGenerator().flow(frames[:1], batch_size=2, seed=1, rank=0, world=2)

@@ -1,8 +1,18 @@
 """Data-parallel rehearsal on ONE GPU: N ranks share device 0 over gloo
-(CNNITMO_DEVICE=0, CNNITMO_DIST_BACKEND=gloo) and run the real engine + the
-bucketed all-reduce (cnn_itmo_amd/dist.py) with different data per rank.  After
-K steps every rank must hold bit-identical parameters, and they must equal a
-single-process replay that averages the ranks' gradients itself.
+(CNNITMO_DEVICE=0, CNNITMO_DIST_BACKEND=gloo) and train through the PUBLIC path
+the reference uses -- paired ImageDataGenerator streams zipped into
+``Model.fit_generator`` (main.py:82-132) with ``distributed=True`` -- so the
+rank-sharded generators, the bucketed all-reduce launched during backward, the
+averaged BN moving statistics and the global epoch logs all run for real.
+
+Checks (rank 0):
+  * every rank ends with bit-identical parameters and moving statistics;
+  * they equal a single-process replay that draws the UNSHARDED stream at the
+    global batch size (batch * world), splits each global batch into the ranks'
+    shares, runs each share with that rank's dropout seed from the same starting
+    state, averages the gradients and the moving statistics itself and applies
+    RMSprop once;
+  * the epoch loss equals the sample-weighted mean of the replay's per-share losses.
 
   CNNITMO_DEVICE=0 CNNITMO_DIST_BACKEND=gloo python -m torch.distributed.run \\
       --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/dp_rehearsal.py
@@ -20,16 +30,18 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import cnn_itmo_amd as C  # noqa: E402
 from cnn_itmo_amd import dist as D  # noqa: E402
+from cnn_itmo_amd import ops  # noqa: E402
+from cnn_itmo_amd.datagen import ImageDataGenerator  # noqa: E402
 
-H, W, B, STEPS = 64, 96, 2, 3
+H, W, B, STEPS, NFR = 64, 96, 2, 3, 11
+AUG = dict(rescale=1. / 255, rotation_range=90, horizontal_flip=True, vertical_flip=True, zoom_range=0.2)
 
 
-def batch(rank, step):
-    g = torch.Generator(device="cuda")
-    g.manual_seed(100 + 7 * rank + 1000 * step)
-    x = torch.rand(B, H, W, 3, generator=g, device="cuda")
-    t = torch.rand(B, H, W, 3, generator=g, device="cuda")
-    return x, t
+def frames():
+    rng = np.random.default_rng(42)
+    x = rng.integers(0, 256, size=(NFR, H, W, 3), dtype=np.uint8)
+    y = rng.integers(0, 256, size=(NFR, H, W, 3), dtype=np.uint8)
+    return x, y
 
 
 def model(dtype):
@@ -42,37 +54,59 @@ def main():
     rank, world, local = D.init_from_env()
     torch.cuda.set_device(local)
     dtype = os.environ.get("DTYPE", "float32")
+    X, Y = frames()
     m = model(dtype)
-    eng = m._engine()
-    b = D.attach(eng, bucket_mb=0.5)  # several buckets, launched during backward
-    for s in range(STEPS):
-        x, t = batch(rank, s)
-        eng.train_step(x, t, seed=s, sync=b.finish, grad_scale=b.grad_scale)
+    if rank != 0:  # rank 0's initial state must win (DDP broadcast)
+        m.set_named_weights({k: v + 0.25 for k, v in m.named_weights().items() if k.endswith("/kernel")})
+    m.distribute(bucket_mb=0.5)  # several buckets, launched during backward
+    gx = ImageDataGenerator(**AUG).flow(X, batch_size=B, seed=1)  # sharded over the group
+    gy = ImageDataGenerator(**AUG).flow(Y, batch_size=B, seed=1)
+    assert (gx.rank, gx.world) == (rank, world)
+    hist = m.fit_generator(zip(gx, gy), steps_per_epoch=STEPS, epochs=1, verbose=0)
+    eng = m.engine
     torch.cuda.synchronize()
     p = eng.params.cpu().numpy()
-    digest = hashlib.sha256(p.tobytes()).hexdigest()
+    bufs = eng.bufs.cpu().numpy()
+    digest = hashlib.sha256(p.tobytes() + bufs.tobytes()).hexdigest()
     out = [None] * world
     dist.all_gather_object(out, digest)
     if rank == 0:
         assert len(set(out)) == 1, f"ranks diverged: {out}"
-        # single-process replay: per-rank gradients averaged by hand, same RMSprop
+        # single-process replay at the global batch size
         r = model(dtype)
         e2 = r._engine()
+        rx = ImageDataGenerator(**AUG).flow(X, batch_size=B * world, seed=1, world=1)
+        ry = ImageDataGenerator(**AUG).flow(Y, batch_size=B * world, seed=1, world=1)
+        lsum, nsum = 0.0, 0
         for s in range(STEPS):
+            xb, yb = next(rx), next(ry)
+            parts = [np.array_split(np.arange(len(xb)), world)[k] for k in range(world)]
             acc = torch.zeros_like(e2.grads)
-            for k in range(world):
-                x, t = batch(k, s)
-                e2.train_step(x, t, seed=s, apply=False)
+            b0 = e2.bufs.clone()
+            bacc = torch.zeros_like(e2.bufs)
+            for k, ix in enumerate(parts):
+                e2.bufs.copy_(b0)
+                ix = torch.as_tensor(ix, device=xb.device)
+                la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False)
+                lsum += float(la[0]) * len(ix)
+                nsum += len(ix)
                 acc += e2.grads
+                bacc += e2.bufs
             e2.step -= world - 1
-            from cnn_itmo_amd import ops
+            e2.bufs.copy_(bacc * (1.0 / world))
             ops.rmsprop(e2.params, acc, e2.accum, 1e-3, 0.9, 1e-7, 1.0 / world)
             e2.weights_dirty = True
         torch.cuda.synchronize()
         q = e2.params.cpu().numpy()
+        qb = e2.bufs.cpu().numpy()
         err = float(np.abs(p - q).max())
-        print(f"dp rehearsal: {world} ranks identical ({out[0][:12]}), max |dp - replay| = {err:.3e}")
+        berr = float(np.abs(bufs - qb).max())
+        lerr = abs(hist.history["loss"][0] - lsum / nsum)
+        print(f"dp rehearsal: {world} ranks identical ({out[0][:12]}), max |dp - replay| params = {err:.3e}, "
+              f"moving stats = {berr:.3e}, epoch loss {hist.history['loss'][0]:.6f} vs {lsum / nsum:.6f}")
         assert err <= 1e-6 * max(1.0, float(np.abs(q).max())), err
+        assert berr <= 1e-6 * max(1.0, float(np.abs(qb).max())), berr
+        assert lerr <= 1e-6 * max(1.0, lsum / nsum), lerr
     dist.barrier()
 
 
