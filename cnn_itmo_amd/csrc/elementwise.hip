@@ -135,8 +135,11 @@ __global__ void bn_fwd_final_kernel(const double* __restrict__ ws, int G, int C,
   smean[c] = (float)mean;
   sinv[c] = (float)inv;
   if (mm && mv) {
-    // Keras 2.2.x: var *= n / (n - (1 + eps)); moving = moving*m + v*(1-m)
-    const double var_u = var * (count / (count - (1.0 + (double)eps)));
+    // Keras 2.2.x on TF 1.x takes tf.nn.fused_batch_norm for 4-D NHWC input, whose
+    // batch variance output is already Bessel-corrected (n/(n-1)); Keras then
+    // multiplies by n/(n-(1+eps)) again before K.moving_average_update:
+    // moving = moving*m + v*(1-m) with v = var_biased * n/(n-1) * n/(n-1-eps).
+    const double var_u = var * (count / (count - 1.0)) * (count / (count - (1.0 + (double)eps)));
     mm[c] = (float)((double)mm[c] * momentum + mean * (1.0 - momentum));
     mv[c] = (float)((double)mv[c] * momentum + var_u * (1.0 - momentum));
   }

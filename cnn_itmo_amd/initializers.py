@@ -14,11 +14,22 @@ def fans(keras_shape):
     return keras_shape[-2] * rf, keras_shape[-1] * rf
 
 
+def truncated_normal(rng, shape):
+    """tf.truncated_normal(0, 1): values beyond 2 standard deviations are re-drawn
+    (not clipped), so the distribution has no point masses and std 0.8796."""
+    z = rng.standard_normal(shape)
+    bad = np.abs(z) > 2.0
+    while bad.any():
+        z[bad] = rng.standard_normal(int(bad.sum()))
+        bad = np.abs(z) > 2.0
+    return z
+
+
 def initialize(kind, keras_shape, rng):
     fan_in, fan_out = fans(keras_shape)
     if kind == "he_normal":
         std = np.sqrt(2.0 / fan_in) / 0.87962566103423978
-        return np.clip(rng.standard_normal(keras_shape), -2.0, 2.0) * std
+        return truncated_normal(rng, keras_shape) * std
     if kind == "glorot_uniform":
         lim = np.sqrt(6.0 / (fan_in + fan_out))
         return rng.uniform(-lim, lim, keras_shape)

@@ -189,9 +189,14 @@ def bn_infer(r, gamma, beta, mmean, mvar, eps=BN_EPS):
 
 
 def bn_moving_update(mmean, mvar, mean, var, count, momentum=BN_MOMENTUM, eps=BN_EPS):
-    """Keras 2.2.x: variance *= n / (n - (1 + eps)) before the moving update;
-    K.moving_average_update: x <- x*momentum + v*(1-momentum)."""
-    var_u = var * (count / (count - (1.0 + eps)))
+    """Moving-statistics update of keras BatchNormalization.call in training
+    [Keras-2.2 + TF-1.x semantics, model.py:196,200]:
+    * K.normalize_batch_in_training takes ``_fused_normalize_batch_in_training``
+      (tf.nn.fused_batch_norm) for 4-D NHWC input; the fused op normalises with the
+      biased variance but RETURNS the Bessel-corrected batch variance n/(n-1)*var;
+    * Keras then applies ``variance *= n / (n - (1 + eps))`` on top;
+    * K.moving_average_update: x <- x*momentum + v*(1-momentum)."""
+    var_u = var * (count / (count - 1.0)) * (count / (count - (1.0 + eps)))
     return mmean * momentum + mean * (1 - momentum), mvar * momentum + var_u * (1 - momentum)
 
 
@@ -256,6 +261,18 @@ UNET_LAYERS = [
 ]
 
 
+def truncated_normal(rng, shape):
+    """tf.truncated_normal(mean 0, stddev 1): standard normal values, every value
+    outside [-2, 2] re-drawn until it falls inside (Keras 2.2 he_normal ->
+    VarianceScaling(distribution='normal') -> K.truncated_normal)."""
+    z = rng.standard_normal(shape)
+    bad = np.abs(z) > 2.0
+    while bad.any():
+        z[bad] = rng.standard_normal(int(bad.sum()))
+        bad = np.abs(z) > 2.0
+    return z
+
+
 def init_unet_params(seed=0, dtype=np.float64):
     """Seeded init with Keras' *distributions* (he_normal truncated, glorot_uniform
     for the head, zero biases, BN gamma=1 beta=0, moving 0/1).  Keras' exact RNG
@@ -267,11 +284,11 @@ def init_unet_params(seed=0, dtype=np.float64):
         if kind == "c3":
             fan_in = 9 * ci
             std = np.sqrt(2.0 / fan_in) / 0.87962566103423978
-            w = np.clip(rng.standard_normal((co, 3, 3, ci)), -2, 2) * std
+            w = truncated_normal(rng, (co, 3, 3, ci)) * std
         elif kind == "t2":
             fan_in = 4 * co  # Keras _compute_fans on (2,2,Cout,Cin): fan_in = Cout*4
             std = np.sqrt(2.0 / fan_in) / 0.87962566103423978
-            w = np.clip(rng.standard_normal((2, 2, co, ci)), -2, 2) * std
+            w = truncated_normal(rng, (2, 2, co, ci)) * std
         else:
             lim = np.sqrt(6.0 / (ci + co))
             w = rng.uniform(-lim, lim, (co, 1, 1, ci))
@@ -471,7 +488,7 @@ def init_tiny_params(seed=0, dtype=np.float64):
     P = {}
     for name, ci, co, k in (("conv2d_1", 3, 32, 3), ("conv2d_2", 32, 32, 3)):
         std = np.sqrt(2.0 / (k * k * ci)) / 0.87962566103423978
-        P[name + "/kernel"] = (np.clip(rng.standard_normal((co, k, k, ci)), -2, 2) * std).astype(dtype)
+        P[name + "/kernel"] = (truncated_normal(rng, (co, k, k, ci)) * std).astype(dtype)
         P[name + "/bias"] = np.zeros(co, dtype)
     lim = np.sqrt(6.0 / (32 + 3))
     P["conv2d_3/kernel"] = rng.uniform(-lim, lim, (3, 1, 1, 32)).astype(dtype)

@@ -203,3 +203,27 @@ def test_tiny_net_grad_vs_torch():
     assert abs(loss - lt.item()) < 1e-12
     for k in g:
         np.testing.assert_allclose(g[k], T[k].grad.numpy(), atol=1e-10, err_msg=k)
+
+
+def test_he_normal_is_truncated_not_clipped():
+    """Keras 2.2 he_normal = VarianceScaling(2, fan_in, 'normal'): a truncated normal
+    (re-drawn beyond 2 sigma) with stddev sqrt(2/fan_in)/0.8796, so the final std is
+    sqrt(2/fan_in) and there is no point mass at the bounds (product and oracle)."""
+    from cnn_itmo_amd import initializers as I
+    rng = np.random.default_rng(0)
+    shp = (3, 3, 256, 256)
+    for w in (I.initialize("he_normal", shp, rng),
+              R.truncated_normal(rng, (256, 3, 3, 256)) * np.sqrt(2.0 / (9 * 256)) / 0.87962566103423978):
+        sig = np.sqrt(2.0 / (9 * 256))
+        bound = 2 * sig / 0.87962566103423978
+        assert np.abs(w).max() <= bound
+        assert np.mean(np.abs(w) > 0.999 * bound) < 1e-3  # no clip mass (clipping would put ~4.6% there)
+        assert abs(w.std() / sig - 1) < 0.01
+
+
+def test_moving_variance_fused_bessel():
+    """Keras-2.2 BN moving variance on TF's fused kernel: n/(n-1) * n/(n-1-eps)."""
+    n, eps = 10.0, 1e-3
+    mm, mv = R.bn_moving_update(np.zeros(1), np.ones(1), np.ones(1), np.full(1, 2.0), n)
+    np.testing.assert_allclose(mv, 0.99 + 0.01 * 2.0 * n / (n - 1) * n / (n - 1 - eps), rtol=1e-15)
+    np.testing.assert_allclose(mm, 0.01, rtol=1e-15)
