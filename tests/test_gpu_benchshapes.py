@@ -1,0 +1,88 @@
+"""Parity at the benchmarked shapes (BASELINE configs[1], [2], [4]): the real
+engine runs one step of each benchmarked workload -- the same model, dtype,
+batch and frame as bench.py -- with every conv / transposed-conv launch checked
+the moment it returns (tests/launch_check.py: sampled fp64 dot products for the
+forward and input-gradient launches incl. the fused BN-backward stores, whole
+fp64 reductions for the weight gradients).  This pins the persistent grids,
+960-column partial strips, 2-GB buffer-descriptor rebasing and 2^31 guards that
+only exist at these sizes.
+
+  configs[2]  1920x1080 (padded 1088), batch 32, bf16 training step
+  configs[1]  1920x1080 (padded 1088), batch 8, fp32 inference (BN moving stats)
+  configs[4]  3840x2160, batch 8 per GPU, bf16 training step (no padding)
+"""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from launch_check import LaunchChecker  # noqa: E402
+
+
+def _run(h, w, batch, dtype, train, expect):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.backends.cuda.matmul.allow_tf32 = False
+    import cnn_itmo_amd as C
+    from cnn_itmo_amd import _lib as L
+    from cnn_itmo_amd import ops
+    C.clear_session()
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = C.U_net(input_size=(h, w, 3), pad=True, dtype=dtype, seed=0, verbose=False)
+    if not train:  # non-trivial moving statistics
+        rng = np.random.default_rng(5)
+        upd = {}
+        for k, v in m.named_weights().items():
+            if k.endswith("/moving_mean"):
+                upd[k] = rng.uniform(0.0, 0.5, v.shape).astype(np.float32)
+            elif k.endswith("/moving_variance"):
+                upd[k] = rng.uniform(0.5, 2.0, v.shape).astype(np.float32)
+        m.set_named_weights(upd)
+    eng = m._engine()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    x = torch.randint(0, 256, (batch, h, w, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+    chk = LaunchChecker(ops, L.BF16 if dtype == "bfloat16" else L.F32)
+    try:
+        if train:
+            t = torch.randint(0, 256, (batch, h, w, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+            la = eng.train_step(x, t, seed=3).cpu().numpy()
+            assert np.isfinite(la).all()
+        else:
+            y = eng.predict(x)
+            assert bool(torch.isfinite(y).all())
+    finally:
+        chk.restore()
+        del eng, m
+        torch.cuda.empty_cache()
+    summ = chk.summary()
+    for (lab, met), v in sorted(summ.items()):
+        print(f"{lab:60s} {met:14s} {v:.3e}")
+    kinds = {lab.split(" ")[0] for lab, _ in summ}
+    missing = set(expect) - kinds
+    assert not missing, f"launch kinds never checked: {missing}"
+
+
+def test_config2_train_1080p_b32_bf16():
+    _run(1080, 1920, 32, "bfloat16", True,
+         ["conv_c3_fwd", "conv3x3_fwd", "tconv_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_dgrad",
+          "tconv_dgrad_bn", "conv_wgrad(9)", "tconv_wgrad", "conv_c3_wgrad"])
+
+
+def test_config1_infer_1080p_b8_f32():
+    _run(1080, 1920, 8, "float32", False, ["im2col_c3", "conv1tap_fwd", "conv3x3_fwd", "tconv_fwd"])
+
+
+def test_config4_train_4k_b8_bf16():
+    _run(2160, 3840, 8, "bfloat16", True,
+         ["conv_c3_fwd", "conv3x3_fwd", "tconv_fwd", "conv3x3_dgrad_bn", "conv_wgrad(9)", "tconv_wgrad"])
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_small_frame_all_launch_kinds(dtype):
+    """The same per-launch checks on a small ragged frame (quick; every kind)."""
+    _run(72, 112, 2, dtype, True, ["conv3x3_fwd", "tconv_fwd", "conv_wgrad(9)", "tconv_wgrad"])
