@@ -309,24 +309,39 @@ def bn_name_for(conv_name):
     return f"batch_normalization_{order.index(conv_name) + 1}"
 
 
+def round_bf16(a):
+    """Round to the nearest bfloat16 (ties to even), returned as float64."""
+    u = np.asarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
 class UNetRef:
     """Forward/backward of the U-Net exactly as model.py:204-278 wires it.
 
     ``bn_groups``: the batch is split into that many equal groups with
     independent BN batch statistics -- the per-replica BN of data parallelism
-    (SURVEY.md 8e)."""
+    (SURVEY.md 8e).
 
-    def __init__(self, params, dtype=np.float64):
+    ``store``: optional rounding applied wherever a tensor is STORED in a
+    reduced-precision pipeline (e.g. ``round_bf16``): the network input, the
+    conv / transposed-conv weights, every post-ReLU activation and BN output,
+    and every input-gradient / pre-activation gradient in the backward.  The
+    arithmetic itself stays in ``dtype``.  It emulates bf16 storage with fp32
+    accumulation, giving the noise floor a bf16 implementation is held to."""
+
+    def __init__(self, params, dtype=np.float64, store=None):
         self.P = {k: np.asarray(v, dtype) for k, v in params.items()}
         self.dtype = dtype
+        self.q = store if store is not None else (lambda a: a)
 
     # ----- building blocks -------------------------------------------------
     def _convbn(self, name, x, training, kind, groups, cache):
         P = self.P
         bn = bn_name_for(name)
-        w, b = P[name + "/kernel"], P[name + "/bias"]
+        w, b = self.q(P[name + "/kernel"]), P[name + "/bias"]
         z = conv2d_same(x, w, b) if kind == "c3" else tconv2x2s2(x, w, b)
-        r = np.maximum(z, 0)
+        r = self.q(np.maximum(z, 0))
         g, be = P[bn + "/gamma"], P[bn + "/beta"]
         if training:
             ys, stats = [], []
@@ -339,12 +354,12 @@ class UNetRef:
             y = bn_infer(r, g, be, P[bn + "/moving_mean"], P[bn + "/moving_variance"])
             stats = None
         cache[name] = dict(x=x, r=r, stats=stats, kind=kind, bn=bn)
-        return y
+        return self.q(y)
 
     def forward(self, x, training=False, seed=0, groups=1, drop_seeds=None):
         """x: [N,H,W,3] in [0,1].  Returns sigmoid output.  ``drop_seeds`` gives
         per-group dropout seeds (default: seed for all groups)."""
-        x = np.asarray(x, self.dtype)
+        x = self.q(np.asarray(x, self.dtype))
         c = {}
         self.cache = c
         self.training = training
@@ -406,15 +421,15 @@ class UNetRef:
         dr = np.concatenate(drs, 0)
         grads[bn + "/gamma"] = np.sum(dgs, 0)
         grads[bn + "/beta"] = np.sum(dbs, 0)
-        dz = dr * (c["r"] > 0)
-        w = P[name + "/kernel"]
+        dz = self.q(dr * (c["r"] > 0))
+        w = self.q(P[name + "/kernel"])
         if c["kind"] == "c3":
             dx, dw, db = conv2d_same_bwd(c["x"], w, dz, need_dx=(name != "conv2d_1"))
         else:
             dx, dw, db = tconv2x2s2_bwd(c["x"], w, dz)
         grads[name + "/kernel"] = dw
         grads[name + "/bias"] = db
-        return dx
+        return None if dx is None else self.q(dx)
 
     def backward(self, target):
         """MSE loss on the last forward; returns (loss, acc, grads)."""

@@ -342,3 +342,71 @@ def test_tconv_dgrad_bn_fused(cin, cout, H, W):
     assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())
     assert np.mean(a != b) < 1e-3
     np.testing.assert_allclose(host(sf), host(sref), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("kind,cin,cout,H,W,c0,c1", [
+    ("c3", 96, 64, 18, 70, 32, 96),     # dec9-style concat [skip 32 | up 64]
+    ("c3", 64, 64, 16, 64, 0, 64),      # whole input (enc chain)
+    ("c3", 192, 128, 16, 32, 64, 192),  # dec8-style
+    ("t2", 128, 64, 3, 70, 0, 128)])    # up9 dgrad into conv8's BN
+def test_dgrad_bn_fused_vs_oracle(kind, cin, cout, H, W, c0, c1):
+    """The fused dgrad + producer-BN-backward pinned DIRECTLY to the oracle:
+    R.conv2d_same_bwd / R.tconv2x2s2_bwd for g, then R.bn_train_bwd and the ReLU
+    mask for the producer's dz.  Coefficients come from the product's
+    cnnitmo_bn_bwd_finalize fed the oracle's sums (sum dy, sum dy*rhat)."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin + cout + H)
+    N, d, c = 2, DT["bf16"], c1 - c0
+    ho, wo = (H, W) if kind == "c3" else (2 * H, 2 * W)
+    if kind == "c3":
+        w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
+    else:
+        w = (rng.standard_normal((2, 2, cout, cin)) * 0.1).astype(np.float32)
+    wr = rnd(w, "bf16")
+    wf = torch.empty(w.size, dtype=torch.bfloat16, device="cuda")
+    wb = torch.empty(w.size, dtype=torch.bfloat16, device="cuda")
+    (ops.prep_conv3x3 if kind == "c3" else ops.prep_tconv)(d, torch.tensor(w).cuda(), cout, cin, wf, wb)
+    dz = rnd(rng.standard_normal((N, ho, wo, cout)), "bf16")
+    r = rnd(np.maximum(rng.standard_normal((N, H, W, c)) + 0.3, 0), "bf16")  # producer post-ReLU
+    gamma = rng.uniform(0.5, 1.5, c)
+    mean, var = r.reshape(-1, c).mean(0), r.reshape(-1, c).var(0)
+    inv = 1.0 / np.sqrt(var + R.BN_EPS)
+    # oracle: consumer input gradient, producer BN backward, ReLU mask
+    if kind == "c3":
+        g = R.conv2d_same_bwd(np.zeros((N, H, W, cin)), wr, dz)[0]
+    else:
+        g = R.tconv2x2s2_bwd(np.zeros((N, H, W, cin)), wr, dz)[0]
+    dy = rnd(g[..., c0:c1], "bf16")  # the fused store applies the BN backward to bf16(g)
+    dr, dgam, dbet = R.bn_train_bwd(dy, r, gamma, mean, var)
+    want = dr * (r > 0)
+    # product: finalize on the oracle's sums -> coef, then the fused kernel
+    rhat = (r - mean) * inv
+    part = np.stack([dy.reshape(-1, c).sum(0), (dy * rhat).reshape(-1, c).sum(0)])[None]  # [1][2][c]
+    coef = torch.empty(3 * c, device="cuda")
+    dgg, dbb = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
+    ops.bn_bwd_finalize(cu(part.astype(np.float32)), 1, c, N * H * W, cu(gamma.astype(np.float32)),
+                        cu(mean.astype(np.float32)), cu(inv.astype(np.float32)), dgg, dbb, coef)
+    rv = dev(r, "bf16").reshape(-1)
+    zf = torch.empty(N * H * W * c, dtype=torch.bfloat16, device="cuda")
+    dzd = dev(dz, "bf16").reshape(-1)
+    if kind == "c3":
+        frows = ops.conv3x3_dgrad_bn_rows(d, N, H, W, cout, cin, c0, c1)
+        whole = c0 == 0 and c1 == cin
+        dx = None if whole else ops.View(torch.zeros(N * H * W * cin, dtype=torch.bfloat16, device="cuda"),
+                                         N, H, W, cin, cin)
+        pf = torch.empty(frows * c, device="cuda")
+        ops.conv3x3_dgrad_bn(d, dzd, N, H, W, cout, wb, cin, dx, c0, c1, coef, rv, zf, pf, False)
+    else:
+        frows = ops.tconv_dgrad_bn_rows(d, N, H, W, cout, cin)
+        pf = torch.empty(frows * c, device="cuda")
+        ops.tconv_dgrad_bn(d, dzd, N, H, W, cout, wb, cin, coef, rv, zf, pf)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(host(dgg), dgam, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(host(dbb), dbet, rtol=1e-5, atol=1e-5)
+    got = host(zf).reshape(want.shape)
+    # bf16 store of an fp32 evaluation (+ one bf16 ulp of g that may round differently)
+    bound = 2.0 ** -8 * np.abs(want) + 2.0 ** -7 * np.abs(gamma * inv * dy) + 1e-3 * np.abs(want).max()
+    assert float((np.abs(got - want) / bound).max()) <= 1.0
+    if kind == "c3" and not (c0 == 0 and c1 == cin):
+        gx = host(dx.buf).reshape(N, H, W, cin)
+        np.testing.assert_allclose(gx[..., :c0], g[..., :c0], rtol=2 ** -7, atol=1e-2 * np.abs(g).max())

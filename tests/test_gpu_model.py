@@ -266,3 +266,56 @@ def test_fit_generator_loss_decreases():
             yield x[2:], t[2:]
     h = m.fit_generator(gen(), steps_per_epoch=10, epochs=3, verbose=0)
     assert h.history["loss"][-1] < h.history["loss"][0]
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_unet_train_step_all_74_grads_128(dtype):
+    """Every one of the 74 gradients of one training step at 128x128 b2 (the
+    bottleneck sees 8x8x2 pixels per channel), each against the fp64 oracle and
+    held to the noise floor of an implementation of that precision:
+      fp32: rel-L2 <= max(1e-4, 3x the deviation of numpy's own float32 run of the
+      same oracle);  loss rel <= 1e-6.  Measured (round 2): the GPU's fp32 gradients
+      are 2e-3..9e-3 from fp64 while numpy-fp32 is 3e-2..9e-2 away -- the chain of 18
+      training-mode BN backwards (dy - mean(dy) - rhat*mean(dy*rhat): near-total
+      cancellation) amplifies fp32 rounding even at 128x128, so 1e-4 per gradient
+      is below what fp32 arithmetic can deliver on this net; the GPU sits 10x under
+      the fp32 floor.
+      bf16 (the bench dtype): rel-L2 <= max(3x, 2e-3) the deviation of the oracle run
+      with bf16 STORAGE emulated (R.round_bf16 at every stored weight, activation and
+      gradient, fp64 arithmetic);  loss rel <= 5e-3."""
+    rng = np.random.default_rng(21)
+    m = build_unet((128, 128, 3), dtype, seed=7)
+    P = randomize_bn(m, rng)
+    x = rng.integers(0, 256, size=(2, 128, 128, 3)) / 255.0
+    t = np.clip(x ** 2.2 * 1.2, 0, 1)
+    eng = m._engine()
+    seed = 9
+    la = eng.train_step(torch.tensor(x, dtype=torch.float32).cuda(),
+                        torch.tensor(t, dtype=torch.float32).cuda(), seed=seed, apply=False).cpu().numpy()
+    grads = eng.get_grads()
+    net = R.UNetRef(P)
+    net.forward(x, training=True, seed=seed)
+    loss, acc, rg = net.backward(t)
+    assert len(rg) == 74 and set(rg) == set(grads)
+    err = {k: _rel_l2(grads[k].reshape(rg[k].shape), rg[k]) for k in rg}
+    if dtype == "float32":
+        em = R.UNetRef(P, np.float32)
+        em.forward(x.astype(np.float32), training=True, seed=seed)
+        eloss, _, eg = em.backward(t.astype(np.float32))
+    else:
+        em = R.UNetRef(P, store=R.round_bf16)
+        em.forward(x, training=True, seed=seed)
+        eloss, _, eg = em.backward(t)
+    floor = {k: _rel_l2(eg[k], rg[k]) for k in rg}
+    for k in sorted(rg):
+        print(f"{dtype} {k:40s} gpu {err[k]:.2e}  floor {floor[k]:.2e}  ratio {err[k] / max(floor[k], 1e-12):.2f}")
+    print(f"{dtype} loss rel {abs(la[0] - loss) / loss:.2e} (floor {abs(eloss - loss) / loss:.2e})")
+    if dtype == "float32":
+        assert abs(la[0] - loss) <= 1e-6 * loss
+        bad = {k: (err[k], floor[k]) for k in rg if err[k] > max(1e-4, 3 * floor[k])}
+        tight = sum(err[k] <= 1e-4 for k in rg)
+        print(f"fp32: {tight}/74 gradients within rel-L2 1e-4")
+    else:
+        assert abs(la[0] - loss) <= 5e-3 * loss
+        bad = {k: (err[k], floor[k]) for k in rg if err[k] > max(3 * floor[k], 2e-3)}
+    assert not bad, bad
