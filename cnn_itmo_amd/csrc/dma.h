@@ -1,0 +1,62 @@
+// LDS-DMA and raw-buffer helpers shared by the LDS-ring kernels (conv_halo,
+// wgrad_halo, wgrad_tconv, tconv_stream).  gfx950 only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace dma {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// voffset at or beyond num_records: a load lands zeros, a store is dropped
+constexpr unsigned OOB = 0x80000000u;
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// raw buffer descriptor over [base, base + 2 GB) from a wave-uniform address
+__device__ __forceinline__ i32x4 rsrc(uintptr_t base) {
+  i32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
+  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xFFFF;
+  r.z = 0x7FFFFFF0;
+  r.w = 0x00020000;
+  return r;
+}
+
+// the same as a __amdgpu_buffer_rsrc_t (for the raw_buffer_load/store builtins)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uintptr_t u = (uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)a) |
+                      ((uintptr_t)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(a >> 32)) << 32);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)u, (short)0, 0x7FFFFFF0, 0x00020000);
+}
+
+// one 16-byte piece per lane -> the wave's 1 KiB LDS image at `lds` (LDS-DMA,
+// lane-linear destination)
+__device__ __forceinline__ void lds16(unsigned voff, i32x4 rs, const char* lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr(lds));
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
+               "s"(a) : "memory");
+}
+
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt takes an immediate: dispatch a wave-uniform count (0..47; larger waits for all)
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+  switch (n) {
+#define W1(k) case k: wait_vm<k>(); break;
+    W1(0) W1(1) W1(2) W1(3) W1(4) W1(5) W1(6) W1(7) W1(8) W1(9) W1(10) W1(11) W1(12) W1(13) W1(14) W1(15)
+    W1(16) W1(17) W1(18) W1(19) W1(20) W1(21) W1(22) W1(23) W1(24) W1(25) W1(26) W1(27) W1(28) W1(29)
+    W1(30) W1(31) W1(32) W1(33) W1(34) W1(35) W1(36) W1(37) W1(38) W1(39) W1(40) W1(41) W1(42) W1(43)
+    W1(44) W1(45) W1(46) W1(47)
+#undef W1
+    default: wait_vm<0>(); break;
+  }
+}
+
+}  // namespace dma

@@ -325,8 +325,8 @@ void set_taps3x3(FwdArgs& a) {
 
 }  // namespace
 
-// conv3x3 forward: the halo kernel writes one row per 256 pixels of each
-// (possibly partial) 8x32 / 8x64 tile, so the count depends on the frame shape.
+// conv3x3 forward: the halo kernel writes one row per (XCD stream, wave), the
+// implicit GEMM one per 256 pixels.
 extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int cin, int cout) {
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
@@ -384,6 +384,7 @@ extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int 
   a.N = dgrad ? cin : cout;
   a.a_ld = a.cin; a.out_ld = a.N;
   a.M = (long)n * h * w;
+  if (!dgrad) a.flags = CNNITMO_RELU;  // the forward epilogue variant (every U-Net conv has one)
   static thread_local char buf[96];
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
