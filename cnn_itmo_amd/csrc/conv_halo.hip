@@ -17,8 +17,9 @@
 // the item it is about to consume.
 //
 // Work distribution (persistent: one 512-thread workgroup per CU, XCD-aware).
-// The dispatcher deals blocks b, b+8, b+16, ... to one XCD.  The workgroups of
-// an XCD form `streams` x `nblocks`: a stream walks a contiguous range of tiles
+// The dispatcher deals blocks b, b+8, b+16, ... to one XCD; xcd_remap numbers
+// them so that each XCD holds a contiguous range of logical ids, and consecutive
+// ids form `streams` groups of `nblocks` workgroups: a stream walks a contiguous range of tiles
 // (image -> column strip -> row, so consecutive tiles share halo rows) and each
 // of its nblocks workgroups computes one BN-column block of every tile.  So the
 // nblocks workgroups of a stream read the same halo at about the same time
@@ -97,11 +98,12 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the vmcnt switch
-  const int xcd = blockIdx.x & 7, xw = blockIdx.x >> 3;
-  const int nb = xw % h.nblocks, sidx = xw / h.nblocks;
-  if (sidx >= h.streams) return;  // the leftover workgroups of an XCD own nothing
-  const int gs = xcd * h.streams + sidx;
-  const long nstr = 8L * h.streams;
+  // logical id: contiguous per XCD (xcd_remap), so a stream's workgroups share one
+  // XCD's L2 except where a stream straddles two XCDs
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int nb = lid % h.nblocks, gs = lid / h.nblocks;
+  if (gs >= h.streams) return;  // the leftover workgroups (< nblocks) own nothing
+  const long nstr = h.streams;
   const long t0 = h.tiles * gs / nstr, t1 = h.tiles * (gs + 1) / nstr;
   const int nch = h.nchunks;
   const long T = (t1 - t0) * nch;
@@ -223,6 +225,20 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // Fragments are double-buffered across taps (tap t+1's ds_reads before tap t's
   // MFMAs, pinned by sched barriers); the next item's DMA pieces go out over the
   // first PFT taps.
+  const int g = lane >> 4, pxl = lane & 15;  // channel group (8 channels per pair) / pixel of the fragment
+
+  // EPI 2: r of the wave's pixels (base at its first pixel; byte offset per (fragment,
+  // pair), OOB for out-of-image pixels and columns outside [c0, c1))
+  auto r_base = [&](const Pos& e) {
+    const long m0 = ((long)e.img * p.ho + e.y0 + wave * RPW) * p.wo + e.x0;
+    return (const bf16*)p.bnb_r + m0 * p.bnb_r_ld + p.bnb_r_off;
+  };
+  auto r_off = [&](const Pos& e, int f, int q) {
+    const int c = n0 + 32 * q + 8 * g;
+    const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
+    const bool ok = e.y0 + wave * RPW + rr < p.ho && e.x0 + col < p.wo && c >= p.bnb_c0 && c < p.bnb_c1;
+    return ok ? (unsigned)((((long)rr * p.wo + col) * p.bnb_r_ld + (c - p.bnb_c0)) * 2) : OOB;
+  };
   auto compute = [&](int buf, bool pf) {
     const char* Ps = smem + buf * STAGE;
     const char* Bs = Ps + C::PATCH;
@@ -255,8 +271,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-
-  const int g = lane >> 4, pxl = lane & 15;  // channel group (8 channels per pair) / pixel of the fragment
   // BN partial sums of the lane's pixels for its 8 channels of each pair (EPI 1), or
   // sums of dz by pixel-row parity (EPI 2; the lane's pixel-column parity is lane & 1)
   constexpr int NSUM = EPI == 0 ? 1 : FP;
@@ -336,19 +350,17 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const int oh0 = e.y0 + wave * RPW;
     const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
     const long m0 = ((long)e.img * p.ho + oh0) * p.wo + e.x0;  // the wave's first pixel
-    const __amdgpu_buffer_rsrc_t rs = dma::brsrc((const bf16*)p.bnb_r + m0 * p.bnb_r_ld + p.bnb_r_off);
+    const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
     dma::i32x4 rv[FM][FP];
 #pragma unroll
     for (int f = 0; f < FM; ++f)
 #pragma unroll
-      for (int q = 0; q < FP; ++q) {
-        const int c = n0 + 32 * q + 8 * g;
-        const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
-        const bool ok = oh0 + rr < p.ho && e.x0 + col < p.wo && c >= c0 && c < c1;
-        const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.bnb_r_ld + (c - c0)) * 2);
-        rv[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? off : OOB, 0, 0);
-      }
-    dma::wait_vm<0>();  // (also retires the next item's DMA, issued during this item's first taps)
+      for (int q = 0; q < FP; ++q) rv[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r_off(e, f, q), 0, 0);
+    // (also retires the next item's DMA, issued during this item's first taps).  Pulling
+    // these pieces into L2 one item ahead by LDS-DMA into the sink measured 15-25 %
+    // slower on every fused dgrad (dec6-dec8), whether issued before or after the
+    // ring's pieces.
+    dma::wait_vm<0>();
     bf16* __restrict__ O = (bf16*)p.out;
     bf16* __restrict__ Z = (bf16*)p.bnb_out;
 #pragma unroll
@@ -412,7 +424,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     __builtin_amdgcn_sched_barrier(0);
     const bool pf = t + ST - 1 < T;
     if (pf) issue_prep(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
-    if (ep.y0 + wave * RPW < p.ho) {
+    const bool act = ep.y0 + wave * RPW < p.ho;
+    if (act) {
       compute(buf, pf);  // issues those loads between its taps
     } else if (pf) {     // the wave's rows are all below the frame: no MFMAs, DMA share only
 #pragma unroll
@@ -546,7 +559,7 @@ void launch_cfg(const HaloArgs& h, int grid, hipStream_t s) {
   hipLaunchKernelGGL((halo_conv_kernel<BN, EPI>), dim3(grid), dim3(NT), 0, s, h);
 }
 
-int halo_streams(const FwdArgs& a, const HaloPlan& pl) { return (halo_ncu() / 8) / (a.N / pl.bn); }
+int halo_streams(const FwdArgs& a, const HaloPlan& pl) { return halo_ncu() / (a.N / pl.bn); }
 
 }  // namespace
 
@@ -566,10 +579,10 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
   h.tiles = (long)a.nimg * h.tiles_x * h.tiles_y;
   h.nblocks = a.N / pl.bn;
   h.streams = halo_streams(a, pl);
-  CNN_REQUIRE(h.streams >= 1, "%s: %d column blocks exceed the workgroups of an XCD", what, h.nblocks);
+  CNN_REQUIRE(h.streams >= 1, "%s: %d column blocks exceed the workgroups", what, h.nblocks);
   CNN_REQUIRE(h.tiles * h.nchunks < (1L << 31), "%s: too many tiles", what);
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
-  const int grid = 8 * (halo_ncu() / 8);
+  const int grid = halo_ncu();
   if (pl.epi == 2) {
     if (pl.bn == 64) launch_cfg<64, 2>(h, grid, s);
     else launch_cfg<32, 2>(h, grid, s);
@@ -595,5 +608,5 @@ const char* halo_name(const FwdArgs& a) {
 long halo_stat_rows(const FwdArgs& a) {
   HaloPlan pl;
   if (!halo_plan(a, pl)) return 0;
-  return 8L * halo_streams(a, pl) * NWAVE;
+  return (long)halo_streams(a, pl) * NWAVE;
 }

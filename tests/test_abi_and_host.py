@@ -44,12 +44,13 @@ def test_queries_without_gpu(lib):
     assert lib.cnnitmo_fwd_stat_rows(1, 1000, 512) == 4
     assert lib.cnnitmo_fwd_stat_rows(1, 1000, 32) in (4, 8)
     assert lib.cnnitmo_border_rows(32) == 32 * 16
-    # conv3x3 (bf16, halo kernel): one row per (XCD stream, wave); without a device the
-    # launcher assumes 256 CUs = 8 XCDs x 32 workgroups; 512 columns = 8 blocks of 64
-    # -> 4 streams per XCD, 8 waves each
+    # conv3x3 (bf16, halo kernel): one row per (stream, wave); without a device the
+    # launcher assumes 256 CUs (one workgroup each); 512 columns = 8 blocks of 64 ->
+    # 32 streams, 768 = 12 blocks -> 21 streams, 8 waves each
     lib.cnnitmo_conv3x3_stat_rows.restype = __import__("ctypes").c_long
-    assert lib.cnnitmo_conv3x3_stat_rows(1, 32, 136, 240, 768, 512) == 8 * 4 * 8
-    assert lib.cnnitmo_conv3x3_stat_rows(1, 32, 1088, 1920, 96, 64) == 8 * 32 * 8
+    assert lib.cnnitmo_conv3x3_stat_rows(1, 32, 136, 240, 768, 512) == 32 * 8
+    assert lib.cnnitmo_conv3x3_stat_rows(1, 32, 136, 240, 512, 768) == 21 * 8
+    assert lib.cnnitmo_conv3x3_stat_rows(1, 32, 1088, 1920, 96, 64) == 256 * 8
     assert lib.cnnitmo_wgrad_workspace_bytes(1, 32, 1088, 1920, 96, 64, 9) > 0
     assert lib.cnnitmo_bn_bwd_rows(1000, 64) >= 1
 

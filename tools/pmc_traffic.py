@@ -37,6 +37,9 @@ def unmangle(n):
 
 def label(name):
     n = unmangle(name.replace(" ", "")).replace("(anonymousnamespace)::", "")
+    m = re.search(r"halo_conv_kernel<(\d+),(\d+)>", n)
+    if m:
+        return "halo_conv_kernel<%s,%s>" % m.groups()
     m = re.search(r"halo_gemm_kernel<(\d+),(\d+),(\d+),(\d+),\d+(?:,(\d+))?>", n)
     if m:
         return "halo_gemm_kernel<%s,%s,%s,%s%s>" % (m.groups()[:4] + (",bnb" if m.group(5) not in (None, "0") else "",))
