@@ -21,45 +21,19 @@
 #include <algorithm>
 #include <cstdio>
 
+#include "dma.h"
 #include "igemm_common.h"
 
 namespace {
 
 #pragma clang diagnostic ignored "-Winline-asm"
-typedef int i32x4 __attribute__((ext_vector_type(4)));
+using dma::i32x4;
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4_ __attribute__((ext_vector_type(4)));
-constexpr unsigned OOB = 0x80000000u;  // voffset beyond num_records: load zeros / drop store
+using dma::OOB;  // voffset beyond num_records: load zeros / drop store
 
-__device__ __forceinline__ unsigned lds_u32(const void* p) {
-  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-}
-__device__ __forceinline__ i32x4 rsrc_of(uintptr_t base) {
-  i32x4 r;
-  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
-  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xFFFF;
-  r.z = 0x7FFFFFF0;
-  r.w = 0x00020000;
-  return r;
-}
-__device__ __forceinline__ void dma16(unsigned voff, i32x4 rs, const char* lds) {
-  const unsigned a = __builtin_amdgcn_readfirstlane(lds_u32(lds));
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
-               "s"(a) : "memory");
-}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t srsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7FFFFFF0, 0x00020000);
-}
-template <int N> __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-__device__ __forceinline__ void vmwait_dyn(int n) {
-  switch (n) {
-#define W1(k) case k: vmwait<k>(); break;
-    W1(0) W1(1) W1(2) W1(3) W1(4) W1(5) W1(6) W1(7) W1(8) W1(9) W1(10) W1(11) W1(12) W1(13) W1(14) W1(15)
-    W1(16) W1(17) W1(18) W1(19) W1(20) W1(21) W1(22) W1(23) W1(24) W1(25) W1(26) W1(27) W1(28) W1(29)
-    W1(30) W1(31)
-#undef W1
-    default: vmwait<0>(); break;
-  }
 }
 // sum over the 16 lanes of each DPP row (lanes = pixels of a fragment): xor 1, xor 2
 // (quad_perm), then half-row and row mirrors; 4 VALU ops, no LDS crossbar traffic
@@ -139,11 +113,11 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   // ---- resident weight block + per-column parameters (once) -------------------
   {
     const int rows = K / 32 * BN;  // 64-byte rows: row = kstep * BN + n
-    const i32x4 rs = rsrc_of((uintptr_t)(p.b + (size_t)n0 * K));
+    const i32x4 rs = dma::rsrc((uintptr_t)(p.b + (size_t)n0 * K));
     for (int q = wave; q < rows / 16; q += 8) {
       const int row = q * 16 + (lane >> 2), piece = (lane & 3) ^ (((row >> 2) & 1) << 1);
       const int ks = row / BN, n = row - ks * BN;
-      dma16((unsigned)((n * K + ks * 32 + piece * 8) * 2), rs, Bres + q * 1024);
+      dma::lds16((unsigned)((n * K + ks * 32 + piece * 8) * 2), rs, Bres + q * 1024);
     }
     for (int c = tid; c < BN; c += C::NT) {
       const int n = n0 + c;
@@ -158,7 +132,7 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
         par[2 * BN + c] = p.coef[2 * p.N + n];
       }
     }
-    vmwait<0>();
+    dma::wait_vm<0>();
     __syncthreads();
   }
 
@@ -190,33 +164,33 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
     tile_pos(t, img, y, x0);
     char* S = ring + slot * STAGE;
     if constexpr (MODE == 0) {
-      const i32x4 rs = rsrc_of((uintptr_t)(p.a + (((size_t)img * p.h + y) * p.w + x0) * p.a_ld + p.a_off + kc * 128));
+      const i32x4 rs = dma::rsrc((uintptr_t)(p.a + (((size_t)img * p.h + y) * p.w + x0) * p.a_ld + p.a_off + kc * 128));
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const bool ok = x0 + apx[i] < p.w;
-        dma16(ok ? (unsigned)((apx[i] * p.a_ld + aks[i] * 32 + apc[i] * 8) * 2) : OOB, rs, S + (wave * 2 + i) * 1024);
+        dma::lds16(ok ? (unsigned)((apx[i] * p.a_ld + aks[i] * 32 + apc[i] * 8) * 2) : OOB, rs, S + (wave * 2 + i) * 1024);
       }
     } else {
-      const i32x4 rs = rsrc_of((uintptr_t)(p.a + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.cout));
+      const i32x4 rs = dma::rsrc((uintptr_t)(p.a + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.cout));
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int k = kc * 128 + aks[i] * 32;  // 32 | cout: the step lies in one tap
         const int tap = k / p.cout, co = k - tap * p.cout;
         const bool ok = x0 + apx[i] < p.w;
         const unsigned off = (unsigned)((((tap >> 1) * W2 + 2 * apx[i] + (tap & 1)) * p.cout + co + apc[i] * 8) * 2);
-        dma16(ok ? off : OOB, rs, S + (wave * 2 + i) * 1024);
+        dma::lds16(ok ? off : OOB, rs, S + (wave * 2 + i) * 1024);
       }
     }
     int n = 2;
     if constexpr (EPI) {
       if (kc == nch - 1) {  // the producer's r tile [64 px][BN] for the fused BN backward
         char* R = rr + (int)((q / nch) & 1) * C::RSLOT;
-        const i32x4 rs = rsrc_of((uintptr_t)(p.r + (((size_t)img * p.h + y) * p.w + x0) * p.r_ld + p.r_off + n0));
+        const i32x4 rs = dma::rsrc((uintptr_t)(p.r + (((size_t)img * p.h + y) * p.w + x0) * p.r_ld + p.r_off + n0));
         for (int j = wave; j < 64 * PPR / 64; j += 8) {  // 1 KB instructions
           const int slot16 = j * 64 + lane, px = slot16 / PPR, sl = slot16 - px * PPR;
           const int pc = sl ^ (px & (PPR - 1));  // piece swizzle by pixel
           const bool ok = x0 + px < p.w;
-          dma16(ok ? (unsigned)((px * p.r_ld + pc * 8) * 2) : OOB, rs, R + j * 1024);
+          dma::lds16(ok ? (unsigned)((px * p.r_ld + pc * 8) * 2) : OOB, rs, R + j * 1024);
         }
         n += (64 * PPR / 64 + 7 - wave) / 8;
       }
@@ -382,7 +356,7 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   mq[ST - 1] = issued;
   int slot = 0;
   for (long q = 0; q < T; ++q) {
-    vmwait_dyn(issued - mq[0]);
+    dma::wait_vm_dyn(issued - mq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);

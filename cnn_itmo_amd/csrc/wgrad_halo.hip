@@ -22,44 +22,15 @@
 #include <cstdio>
 #include <cstring>
 
+#include "dma.h"
 #include "igemm_common.h"
 
 #pragma clang diagnostic ignored "-Winline-asm"
 
 namespace {
 
-__device__ __forceinline__ unsigned lds_addr3(const void* p) {
-  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-}
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-// raw buffer descriptor over [base, base + 2 GB): loads at voffset >= OOB_OFF are
-// dropped by the range check and land zeros (image edges, overhanging strips)
-constexpr unsigned OOB_OFF = 0x80000000u;
-__device__ __forceinline__ i32x4 buf_rsrc(uintptr_t base) {
-  i32x4 r;
-  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
-  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xFFFF;
-  r.z = 0x7FFFFFF0;
-  r.w = 0x00020000;
-  return r;
-}
-__device__ __forceinline__ void blds(unsigned voff, i32x4 rs, const char* lds) {
-  const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr3(lds));
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
-               "s"(a) : "memory");
-}
-template <int N> __device__ __forceinline__ void waitvm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-__device__ __forceinline__ void waitvm_dyn(int n) {
-  switch (n) {
-#define W1(k) case k: waitvm<k>(); break;
-    W1(0) W1(1) W1(2) W1(3) W1(4) W1(5) W1(6) W1(7) W1(8) W1(9) W1(10) W1(11) W1(12) W1(13) W1(14) W1(15)
-    W1(16) W1(17) W1(18) W1(19) W1(20) W1(21) W1(22) W1(23) W1(24) W1(25) W1(26) W1(27) W1(28) W1(29)
-    W1(30) W1(31) W1(32) W1(33) W1(34) W1(35) W1(36) W1(37) W1(38) W1(39) W1(40) W1(41) W1(42) W1(43)
-    W1(44) W1(45) W1(46) W1(47)
-#undef W1
-    default: waitvm<0>(); break;
-  }
-}
+using dma::i32x4;
+
 
 // row swizzle of the 32-byte column blocks of an R-channel bf16 row
 template <int R> __device__ __forceinline__ int trswz(int row) {
@@ -129,7 +100,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 
   // ---- per-lane DMA geometry (fixed for the launch) --------------------------
   // x row image: XROWS pixel rows (columns x0-1 .. x0+TW) of BN channels
-  unsigned xoff[LX];  // byte offset from pixel (row g, column x0 - 1), OOB_OFF outside the image
+  unsigned xoff[LX];  // byte offset from pixel (row g, column x0 - 1), dma::OOB outside the image
   bool xact[LX];      // this wave issues DMA q
 #pragma unroll
   for (int q = 0; q < LX; ++q) {
@@ -139,7 +110,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     const int row = off / (BN * 2), pos = off - row * (BN * 2);
     const int col = (((pos >> 5) ^ trswz<BN>(row)) << 4) + ((pos >> 4) & 1) * 8;
     const int xx = x0 - 1 + row;
-    xoff[q] = row < C::XROWS && xx >= 0 && xx < p.W ? (unsigned)((row * p.x_ld + col) * 2) : OOB_OFF;
+    xoff[q] = row < C::XROWS && xx >= 0 && xx < p.W ? (unsigned)((row * p.x_ld + col) * 2) : dma::OOB;
   }
   unsigned doff[LD];
   bool dact[LD];  // (the last strip may overhang the image: zero columns)
@@ -150,7 +121,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     const int off = ins * 1024 + lane * 16;
     const int row = off / (BM * 2), pos = off - row * (BM * 2);
     const int col = (((pos >> 5) ^ trswz<BM>(row)) << 4) + ((pos >> 4) & 1) * 8;
-    doff[q] = x0 + row < p.W ? (unsigned)((row * p.cout + col) * 2) : OOB_OFF;
+    doff[q] = x0 + row < p.W ? (unsigned)((row * p.cout + col) * 2) : dma::OOB;
   }
   int nx = 0, nd = 0;  // DMA instructions this wave issues per x / dz row
 #pragma unroll
@@ -162,17 +133,17 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     char* S = xbase + slot * XB * 1024;
     const bool ok = g >= 0 && g < total_rows;
     const long e0 = ((long)g * p.W + x0 - 1) * p.x_ld + p.x_off + n0;  // may be < 0 (first pixel)
-    const i32x4 rs = buf_rsrc((uintptr_t)p.x + (uintptr_t)(e0 * 2));
+    const i32x4 rs = dma::rsrc((uintptr_t)p.x + (uintptr_t)(e0 * 2));
 #pragma unroll
     for (int q = 0; q < LX; ++q)
-      if (xact[q]) blds(ok ? xoff[q] : OOB_OFF, rs, S + (wave + q * NW) * 1024);
+      if (xact[q]) dma::lds16(ok ? xoff[q] : dma::OOB, rs, S + (wave + q * NW) * 1024);
   };
   auto issue_d = [&](long g, int slot) {
     char* S = dbase + slot * DB * 1024;
-    const i32x4 rs = buf_rsrc((uintptr_t)(p.dz + ((size_t)g * p.W + x0) * p.cout + m0));
+    const i32x4 rs = dma::rsrc((uintptr_t)(p.dz + ((size_t)g * p.W + x0) * p.cout + m0));
 #pragma unroll
     for (int q = 0; q < LD; ++q)
-      if (dact[q]) blds(doff[q], rs, S + (wave + q * NW) * 1024);
+      if (dact[q]) dma::lds16(doff[q], rs, S + (wave + q * NW) * 1024);
   };
 
   f32x4 acc[3][FM][FN];  // taps (wr, s), s = 0..2
@@ -215,7 +186,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
   int ds0 = 0;  // slot of dz row g0+k
   int y = (int)(g0 % p.H);
   for (int k = 0; k < nrows; ++k) {
-    waitvm_dyn(issued - mq[0]);
+    dma::wait_vm_dyn(issued - mq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);

@@ -25,31 +25,15 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "dma.h"
 #include "igemm_common.h"
 
 #pragma clang diagnostic ignored "-Winline-asm"
 
 namespace {
 
-__device__ __forceinline__ unsigned lds_addr3(const void* p) {
-  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-}
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-constexpr unsigned OOB_OFF = 0x80000000u;
-__device__ __forceinline__ i32x4 buf_rsrc(uintptr_t base) {
-  i32x4 r;
-  r.x = __builtin_amdgcn_readfirstlane((int)(unsigned)base);
-  r.y = __builtin_amdgcn_readfirstlane((int)(unsigned)(base >> 32)) & 0xFFFF;
-  r.z = 0x7FFFFFF0;
-  r.w = 0x00020000;
-  return r;
-}
-__device__ __forceinline__ void blds(unsigned voff, i32x4 rs, const char* lds) {
-  const unsigned a = __builtin_amdgcn_readfirstlane(lds_addr3(lds));
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
-               "s"(a) : "memory");
-}
-template <int N> __device__ __forceinline__ void waitvm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+using dma::i32x4;
+
 
 template <int R> __device__ __forceinline__ int trswz(int row) {
   if constexpr (R == 64) return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
@@ -121,7 +105,7 @@ __global__ __launch_bounds__(2 * (BM / 64) * (BN / 64) * 64) void wgrad_tconv_ke
     const int off = (wave + q * NW) * 1024 + lane * 16;
     const int row = off / (BN * 2), pos = off - row * (BN * 2);
     const int col = (((pos >> 5) ^ trswz<BN>(row)) << 4) + ((pos >> 4) & 1) * 8;
-    xoff[q] = x0 + row < p.W ? (unsigned)((row * p.x_ld + col) * 2) : OOB_OFF;
+    xoff[q] = x0 + row < p.W ? (unsigned)((row * p.x_ld + col) * 2) : dma::OOB;
   }
 #pragma unroll
   for (int q = 0; q < QD; ++q) {
@@ -132,19 +116,19 @@ __global__ __launch_bounds__(2 * (BM / 64) * (BN / 64) * 64) void wgrad_tconv_ke
     const int col = (((pos >> 5) ^ trswz<BM>(row)) << 4) + ((pos >> 4) & 1) * 8;
     const int b = row / TW, k = row - b * TW;  // image row b*TW + k <- column 2k+b
     // a selects the second dy row: one row is 2W pixels further
-    doff[q] = x0 + k < p.W ? (unsigned)((((long)a * 2 * p.W + 2 * k + b) * p.cout + col) * 2) : OOB_OFF;
+    doff[q] = x0 + k < p.W ? (unsigned)((((long)a * 2 * p.W + 2 * k + b) * p.cout + col) * 2) : dma::OOB;
   }
 
   auto issue = [&](long g, int slot) {
     char* S = smem + slot * C::SLOT;
     const bool ok = g < g1;
     const long gg = ok ? g : g0;
-    const i32x4 rx = buf_rsrc((uintptr_t)(p.x + ((size_t)gg * p.W + x0) * p.x_ld + p.x_off + n0));
+    const i32x4 rx = dma::rsrc((uintptr_t)(p.x + ((size_t)gg * p.W + x0) * p.x_ld + p.x_off + n0));
 #pragma unroll
-    for (int q = 0; q < QX; ++q) blds(ok ? xoff[q] : OOB_OFF, rx, S + (wave + q * NW) * 1024);
-    const i32x4 rd = buf_rsrc((uintptr_t)(p.dy + ((size_t)(2 * gg) * 2 * p.W + 2 * x0) * p.cout + m0));
+    for (int q = 0; q < QX; ++q) dma::lds16(ok ? xoff[q] : dma::OOB, rx, S + (wave + q * NW) * 1024);
+    const i32x4 rd = dma::rsrc((uintptr_t)(p.dy + ((size_t)(2 * gg) * 2 * p.W + 2 * x0) * p.cout + m0));
 #pragma unroll
-    for (int q = 0; q < QD; ++q) blds(ok ? doff[q] : OOB_OFF, rd, S + (XB + wave + q * NW) * 1024);
+    for (int q = 0; q < QD; ++q) dma::lds16(ok ? doff[q] : dma::OOB, rd, S + (XB + wave + q * NW) * 1024);
   };
 
   f32x4 acc[2][FM][FN];
@@ -160,7 +144,7 @@ __global__ __launch_bounds__(2 * (BM / 64) * (BN / 64) * 64) void wgrad_tconv_ke
   for (int k = 0; k < D; ++k) issue(g0 + k, k);
   int slot = 0, nslot = D;
   for (int k = 0; k < nrows; ++k) {
-    waitvm<D * PER - PER>();  // this step's group landed (D-1 younger groups may fly)
+    dma::wait_vm<D * PER - PER>();  // this step's group landed (D-1 younger groups may fly)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -199,7 +183,7 @@ __global__ __launch_bounds__(2 * (BM / 64) * (BN / 64) * 64) void wgrad_tconv_ke
     slot = slot + 1 == C::S ? 0 : slot + 1;
     nslot = nslot + 1 == C::S ? 0 : nslot + 1;
   }
-  waitvm<0>();  // run-out loads (zeros) drain before the workgroup ends
+  dma::wait_vm<0>();  // run-out loads (zeros) drain before the workgroup ends
 
   // ---- this workgroup's slab: [4*cout][cin], row = (2a+b)*cout + co ----------
   float* __restrict__ O = p.out + (size_t)unit * p.slab;

@@ -231,19 +231,27 @@ def build_from_config(cfg, seed=0):
     return Model(inputs=built[inp], outputs=built[out], name=c.get("name", "model_1"), seed=seed)
 
 
-def _read_weights(model, g):
-    """Keras load_weights_from_hdf5_group: layers matched by name, weights in order."""
+def _read_weights(model, g, by_name=False):
+    """Keras 2.2 load_weights_from_hdf5_group: the file's layers with weights are
+    matched to the model's layers with weights by POSITION (topological order; layer
+    names may differ, e.g. when other models were built earlier in the session), the
+    weights of a layer in order.  by_name=True (load_weights_from_hdf5_group_by_name):
+    matched by layer name instead; file layers without a model layer of that name
+    are skipped."""
     from .model import _to_internal
     names = _attr_chunks(g, "layer_names")
-    by_name = {l.name: l for l in model.layers}
     named = {}
     with_w = [n for n in names if _attr_chunks(g[n], "weight_names")]
-    model_w = [l for l in model.layers if l.weight_shapes()]
-    if len(with_w) != len(model_w):
-        raise ValueError(f"You are trying to load a weight file containing {len(with_w)} layers into a model "
-                         f"with {len(model_w)} layers.")
-    for fname, ml in zip(with_w, model_w):
-        l = by_name.get(fname, ml)  # by name when it exists, else by position (Keras topological load)
+    if by_name:
+        by = {l.name: l for l in model.layers if l.weight_shapes()}
+        pairs = [(n, by[n]) for n in with_w if n in by]
+    else:
+        model_w = [l for l in model.layers if l.weight_shapes()]
+        if len(with_w) != len(model_w):
+            raise ValueError(f"You are trying to load a weight file containing {len(with_w)} layers into a "
+                             f"model with {len(model_w)} layers.")
+        pairs = list(zip(with_w, model_w))
+    for fname, l in pairs:
         lg = g[fname]
         wn = _attr_chunks(lg, "weight_names")
         shapes = l.weight_shapes()
@@ -257,9 +265,9 @@ def _read_weights(model, g):
     model.set_named_weights(named)
 
 
-def load_weights_hdf5(model, path):
+def load_weights_hdf5(model, path, by_name=False):
     f = hdf5.File(path)
-    _read_weights(model, f["model_weights"] if "model_weights" in f else f.root)
+    _read_weights(model, f["model_weights"] if "model_weights" in f else f.root, by_name=by_name)
 
 
 def load_model_hdf5(path, compile=True):

@@ -452,11 +452,13 @@ class Model:
             return
         self.save(path, include_optimizer=False)
 
-    def load_weights(self, path):
+    def load_weights(self, path, by_name=False):
+        """keras Model.load_weights: HDF5 weights are matched topologically (file layer k
+        -> k-th model layer with weights), or by layer name with ``by_name=True``."""
         from . import hdf5
         if hdf5.is_hdf5(path):
             from . import keras_h5
-            keras_h5.load_weights_hdf5(self, path)
+            keras_h5.load_weights_hdf5(self, path, by_name=by_name)
             return
         with np.load(path, allow_pickle=False) as z:
             self.set_named_weights({k[2:]: z[k] for k in z.files if k.startswith("w/")})

@@ -126,6 +126,25 @@ def test_save_weights_load_weights_h5(tmp_path):
     _same_weights(a.named_weights(), b.named_weights())
 
 
+def test_load_weights_topological_with_shifted_names(tmp_path):
+    """Keras 2.2 load_weights(by_name=False) is positional: a model whose layer names
+    are shifted (another model was built earlier in the session) still loads; by_name=True
+    matches names and skips the file layers the model does not have."""
+    C.clear_session()
+    a = C.TinyNet(seed=1)  # conv2d_1..3
+    p = tmp_path / "w.h5"
+    a.save_weights(str(p))
+    b = C.TinyNet(seed=2)  # same session: conv2d_4..6
+    assert {l.name for l in a.layers}.isdisjoint({l.name for l in b.layers} - {"input_1", "input_2"})
+    b.load_weights(str(p))
+    for (ka, va), (kb, vb) in zip(sorted(a.named_weights().items()), sorted(b.named_weights().items())):
+        assert np.array_equal(va, vb), (ka, kb)
+    c = C.TinyNet(seed=3)
+    before = {k: v.copy() for k, v in c.named_weights().items()}
+    c.load_weights(str(p), by_name=True)  # no layer names in common: nothing changes
+    _same_weights(before, c.named_weights())
+
+
 def test_mismatched_file_raises(tmp_path):
     C.clear_session()
     a = C.TinyNet(seed=1)
