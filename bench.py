@@ -82,7 +82,7 @@ class KernelTimer:
         bn = 128 if n % 128 == 0 else 64 if n % 64 == 0 else 96 if n % 96 == 0 else 32
         return f"igemm_fwd2_kernel<{t},256x{bn}>"
 
-    def _bracket(self, name, flops, fn, *a, **k):
+    def _bracket(self, name, flops, tag, fn, *a, **k):
         if not self.on:
             return fn(*a, **k)
         i = self._next
@@ -93,7 +93,7 @@ class KernelTimer:
         e0.record()
         r = fn(*a, **k)
         e1.record()
-        self.rec.append((name, flops, e0, e1))
+        self.rec.append((name, flops, e0, e1, tag))
         return r
 
     def reset(self):
@@ -112,49 +112,49 @@ class KernelTimer:
 
         def conv3x3_fwd(dt, x, wt, bias, out, *a, **k):
             fl = 2.0 * x.p * out.c * 9 * x.c
-            return self._bracket(kname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, o["conv3x3_fwd"], dt, x, wt, bias,
+            return self._bracket(kname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, f"fwd {x.h}x{x.w} {x.c}->{out.c}", o["conv3x3_fwd"], dt, x, wt, bias,
                                  out, *a, **k)
 
         def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx):
             fl = 2.0 * n * h * w * cin * 9 * cout
-            return self._bracket(kname(dt, n, h, w, cin, cout, 1), fl, o["conv3x3_dgrad"], dt, dz, n, h, w, cout,
+            return self._bracket(kname(dt, n, h, w, cin, cout, 1), fl, f"dgrad {h}x{w} {cout}->{cin}", o["conv3x3_dgrad"], dt, dz, n, h, w, cout,
                                  wflip, cin, dx)
 
         def conv3x3_dgrad_bn(dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1, *a, **k):
             fl = 2.0 * n * h * w * cin * 9 * cout
             name = query("cnnitmo_conv3x3_dgrad_bn_kernel_name", dt, n, h, w, cout, cin, c0, c1).decode()
-            return self._bracket(name, fl, o["conv3x3_dgrad_bn"], dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1,
+            return self._bracket(name, fl, f"dgrad_bn {h}x{w} {cout}->{cin}[{c0}:{c1}]", o["conv3x3_dgrad_bn"], dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1,
                                  *a, **k)
 
         def tconv_dgrad_bn(dt, dout, n, h, w, cout, kT, cin, *a, **k):
             fl = 2.0 * n * h * w * cin * 4 * cout
             name = query("cnnitmo_tconv2x2_dgrad_bn_kernel_name", dt, n, h, w, cout, cin).decode()
-            return self._bracket(name, fl, o["tconv_dgrad_bn"], dt, dout, n, h, w, cout, kT, cin, *a, **k)
+            return self._bracket(name, fl, f"t.dgrad_bn {h}x{w} {cout}->{cin}", o["tconv_dgrad_bn"], dt, dout, n, h, w, cout, kT, cin, *a, **k)
 
         def tname(dt, n, h, w, cin, cout, dgrad):
             return query("cnnitmo_tconv2x2_kernel_name", dt, n, h, w, cin, cout, dgrad).decode()
 
         def tconv_fwd(dt, x, k_, bias, out, *a, **k):
             fl = 2.0 * x.p * 4 * out.c * x.c
-            return self._bracket(tname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, o["tconv_fwd"], dt, x, k_, bias, out,
+            return self._bracket(tname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, f"t.fwd {x.h}x{x.w} {x.c}->{out.c}", o["tconv_fwd"], dt, x, k_, bias, out,
                                  *a, **k)
 
         def tconv_dgrad(dt, dout, n, h, w, cout, kT, cin, dx):
             fl = 2.0 * n * h * w * cin * 4 * cout
-            return self._bracket(tname(dt, n, h, w, cin, cout, 1), fl, o["tconv_dgrad"], dt, dout, n, h, w, cout,
+            return self._bracket(tname(dt, n, h, w, cin, cout, 1), fl, f"t.dgrad {h}x{w} {cout}->{cin}", o["tconv_dgrad"], dt, dout, n, h, w, cout,
                                  kT, cin, dx)
 
         def conv1tap_fwd(dt, cols, kk, m, wt, bias, out, *a, **k):
             fl = 2.0 * m * out.c * 27  # algorithmic K = 3x3x3 (the packed 32 has 5 zero columns)
-            return self._bracket(self.fwd_name(dt, out.c), fl, o["conv1tap_fwd"], dt, cols, kk, m, wt, bias, out, *a, **k)
+            return self._bracket(self.fwd_name(dt, out.c), fl, "c3in fwd", o["conv1tap_fwd"], dt, cols, kk, m, wt, bias, out, *a, **k)
 
         def conv_c3_fwd(x, n, hv, h, w, *a, **k):
             fl = 2.0 * n * h * w * 32 * 27
-            return self._bracket("conv_c3_fwd_kernel", fl, o["conv_c3_fwd"], x, n, hv, h, w, *a, **k)
+            return self._bracket("conv_c3_fwd_kernel", fl, "c3 fwd", o["conv_c3_fwd"], x, n, hv, h, w, *a, **k)
 
         def conv_c3_wgrad(x, n, hv, h, w, *a, **k):
             fl = 2.0 * n * h * w * 32 * 27
-            return self._bracket("conv_c3_wgrad_kernel + fold", fl, o["conv_c3_wgrad"], x, n, hv, h, w, *a, **k)
+            return self._bracket("conv_c3_wgrad_kernel + fold", fl, "c3 wgrad", o["conv_c3_wgrad"], x, n, hv, h, w, *a, **k)
 
         def wname(dt, ntaps, n, h, w, cin, cout):
             k = query("cnnitmo_wgrad_kernel_name", dt, ntaps, n, h, w, cin, cout).decode()
@@ -162,12 +162,12 @@ class KernelTimer:
 
         def conv_wgrad(dt, ntaps, x, dz, cout, dw, *a, **k):
             fl = 2.0 * x.p * cout * (27 if ntaps == 1 else 9 * x.c)
-            return self._bracket(wname(dt, ntaps, x.n, x.h, x.w, x.c, cout), fl, o["conv_wgrad"],
+            return self._bracket(wname(dt, ntaps, x.n, x.h, x.w, x.c, cout), fl, f"wgrad {x.h}x{x.w} {x.c}->{cout}", o["conv_wgrad"],
                                  dt, ntaps, x, dz, cout, dw, *a, **k)
 
         def tconv_wgrad(dt, x, dout, cout, dk, *a, **k):
             fl = 2.0 * x.p * 4 * cout * x.c
-            return self._bracket(wname(dt, 4, x.n, x.h, x.w, x.c, cout), fl, o["tconv_wgrad"],
+            return self._bracket(wname(dt, 4, x.n, x.h, x.w, x.c, cout), fl, f"t.wgrad {x.h}x{x.w} {x.c}->{cout}", o["tconv_wgrad"],
                                  dt, x, dout, cout, dk, *a, **k)
 
         for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad),
@@ -176,9 +176,19 @@ class KernelTimer:
                      ("tconv_wgrad", tconv_wgrad), ("conv_c3_fwd", conv_c3_fwd), ("conv_c3_wgrad", conv_c3_wgrad)):
             setattr(ops, n, f)
 
+    def detail(self):
+        """(name, launch tag) -> [launches, flops, ms]: per-layer view of the same events."""
+        agg = {}
+        for name, fl, e0, e1, tag in self.rec:
+            a = agg.setdefault((name, tag), [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += fl
+            a[2] += e0.elapsed_time(e1)
+        return agg
+
     def summary(self):
         agg = {}
-        for name, fl, e0, e1 in self.rec:
+        for name, fl, e0, e1, _ in self.rec:
             ms = e0.elapsed_time(e1)
             a = agg.setdefault(name, [0, 0.0, 0.0])
             a[0] += 1
@@ -284,6 +294,13 @@ def _print_agg(agg, tag):
               file=sys.stderr)
 
 
+def _print_detail(det, steps, tag):
+    """Per launch site (kernel, layer shape): ms per step and TFLOP/s."""
+    for (k, t), (c, f, m) in sorted(det.items(), key=lambda kv: -kv[1][2]):
+        print(f"[bench:{tag}:site] {m / steps:7.3f} ms/step {f / (m * 1e-3) / 1e12:7.1f} TF/s  {k:42s} {t}",
+              file=sys.stderr)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -378,6 +395,7 @@ def main():
     roof["timed_pass_ms_per_step"] = round(elapsed2 / k2 * 1e3, 2)
     if rank == 0:
         _print_agg(agg, args.mode)
+        _print_detail(timer.detail(), k2, args.mode)
         if losses and losses[-1] is not None:
             print(f"[bench] last loss/acc: {losses[-1].cpu().numpy().tolist()}", file=sys.stderr)
         print(f"[bench] peak mem {torch.cuda.max_memory_allocated() / 2**30:.1f} GiB, "
