@@ -19,7 +19,8 @@ runs on (its ms/step is reported beside).  `allreduce_exposed` (N>1) is the time
 the compute stream waits for the RCCL buckets after backward.  `cpu_baseline`
 times this repo's numpy oracle (oracle/unet_ref.py) on the host (rank 0, N=1).
 `fp32_infer` is BASELINE configs[1] (1080p b8 fp32 inference) with its own
-roofline and CPU baseline.
+roofline and CPU baseline; `k4_train` is configs[4] (3840x2160, bf16 training,
+8 frames per GPU = global 64 on 8 GPUs).
 """
 from __future__ import annotations
 
@@ -57,6 +58,9 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=16.0)
     ap.add_argument("--infer-batch", type=int, default=8,
                     help="fp32 inference leg (configs[1]) frames per GPU; 0 = skip")
+    ap.add_argument("--k4-batch", type=int, default=8,
+                    help="4K bf16 training leg (configs[4]: 3840x2160, global 64 on 8 GPUs) frames per GPU; 0 = skip")
+    ap.add_argument("--k4-steps", type=int, default=4)
     return ap.parse_args()
 
 
@@ -419,13 +423,19 @@ def main():
             cpu = {"error": repr(e)}
 
     # configs[1]: fp32 inference leg (b8 1080p, BN moving stats), same ranks, weak
-    infer = None
-    if args.mode == "train" and args.infer_batch > 0:
+    infer = k4 = None
+    if args.mode == "train" and (args.infer_batch > 0 or args.k4_batch > 0):
         del eng, model, x, t, losses
         timer.rec = []
         C.clear_session()
         torch.cuda.empty_cache()
+    if args.mode == "train" and args.infer_batch > 0:
         infer = infer_leg(args, rank, world, timer, barrier, P_init, H, W)
+        C.clear_session()
+        torch.cuda.empty_cache()
+    # configs[4]: 4K training (b8 per GPU = global 64 on 8 GPUs), DP when N > 1
+    if args.mode == "train" and args.k4_batch > 0:
+        k4 = k4_leg(args, rank, world, barrier)
 
     if rank == 0:
         res = "1080p" if (args.height, args.width) == (1080, 1920) else f"{args.width}x{args.height}"
@@ -446,6 +456,8 @@ def main():
             line["replicas"] = replicas
         if infer is not None:
             line["fp32_infer"] = infer
+        if k4 is not None:
+            line["k4_train"] = k4
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -520,6 +532,59 @@ def infer_leg(args, rank, world, timer, barrier, P_init, H, W):
                 out["cpu_baseline"] = {"error": repr(e)}
     del eng, m, x, yhat
     return out
+
+
+def k4_leg(args, rank, world, barrier):
+    """BASELINE configs[4]: 3840x2160 frames, bf16, fwd+bwd+RMSprop, k4_batch frames per
+    GPU (8 = global 64 on 8 GPUs), DP over the same ranks when N > 1.  The activations
+    are not tiled: at 8 frames per GPU the step's working set fits one GPU's HBM
+    (peak_mem_gib), so the frame is processed whole, which keeps every pixel's
+    receptive field exact."""
+    import torch
+    import cnn_itmo_amd as C
+    Hk, Wk = 2160, 3840
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = C.U_net(input_size=(Hk, Wk, 3), pad=True, dtype="bfloat16", seed=0, verbose=False)
+    eng = m._engine()
+    dp = None
+    if world > 1:
+        m.distribute(bucket_mb=args.bucket_mb)
+        dp = m._dp
+    B = args.k4_batch
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4321 + 7919 * rank)
+    x = torch.randint(0, 256, (B, Hk, Wk, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+    t = torch.randint(0, 256, (B, Hk, Wk, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+    opt = m.optimizer
+    torch.cuda.reset_peak_memory_stats()
+
+    def step(i):
+        kw = dict(seed=i * world + rank, lr=opt.lr, rho=opt.rho, eps=opt.epsilon)
+        if dp is not None:
+            kw.update(sync=dp.finish, grad_scale=dp.grad_scale)
+        return eng.train_step(x, t, **kw)
+
+    for i in range(max(1, min(args.warmup, 2))):
+        step(i)
+    k = max(1, args.k4_steps)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(k):
+        out = step(100 + i)
+    barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = el.item()
+    loss = out.cpu().numpy().tolist() if out is not None else None
+    res = {"metric": "4K SDR->HDR frames/sec (fwd+bwd)", "value": round(B * world * k / elapsed, 3),
+           "unit": "frames/s", "dtype": "bf16", "steps": k, "ms_per_step": round(elapsed / k * 1e3, 2),
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1), "last_loss_acc": loss,
+           "config": {"workload": f"U-Net train step, {Wk}x{Hk} frames, {B} frames/GPU (BASELINE configs[4]; "
+                                  f"whole frames, no spatial tiling needed)", "global_batch": B * world,
+                      "parallelism": f"dp{world}"}}
+    del eng, m, x, t
+    return res
 
 
 if __name__ == "__main__":
