@@ -7,5 +7,5 @@ R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc_$c" -o run -- \
-    python3 "$R/bench.py" --no-cpu --steps 1 --warmup 0 > "$R/gpurun_out/pmc_$c.log" 2>&1
+    python3 "$R/bench.py" --no-cpu --steps 1 --warmup 0 --k4-batch 0 > "$R/gpurun_out/pmc_$c.log" 2>&1
 done
