@@ -85,7 +85,9 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the vmcnt switch
   const int wr = wave / C::NWG, wq = wave - wr * C::NWG;  // kernel row of this wave's taps
   const int wm = wq / WN, wn = wq % WN;
-  int bid = blockIdx.x;
+  // consecutive logical ids (the cbm x cbn column blocks of one strip and row range,
+  // which read the same dz / x rows) run on one XCD: the re-reads are L2 hits
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int cb = bid % (p.cbm * p.cbn);
   bid /= p.cbm * p.cbn;
   const int strip = bid % p.strips;
