@@ -30,7 +30,7 @@
 //
 // MFMA 16x16x32 bf16 with the operands swapped (C^T = W^T X^T): a lane ends up
 // with one pixel and 4 consecutive channels per fragment.  The weight rows are
-// permuted inside each 32-column pair of fragments (hperm) so that a lane's
+// permuted inside each 32-column pair of fragments (pair_perm, igemm_common.h) so that a lane's
 // two fragments hold 8 CONSECUTIVE channels: one 16-byte store per (pixel, 8
 // channels) straight from registers, no C tile in LDS, no barrier in the
 // epilogue.
@@ -74,12 +74,6 @@ template <int BN> struct HCfg {
   static_assert(BN % 32 == 0, "column pairs");
 };
 
-// LDS weight row nn (fragment nn/16, MFMA row nn%16) holds column hperm(nn) of the
-// block: lane group g of the fragment pair (2p, 2p+1) then owns columns
-// 32p + 8g .. +7 (4 in each fragment).
-__host__ __device__ constexpr int hperm(int nn) {
-  return 32 * (nn >> 5) + 8 * ((nn & 15) >> 2) + 4 * ((nn >> 4) & 1) + (nn & 3);
-}
 
 // store sink for EPI 2's out-of-image pixels (global stores, fixed count per wave)
 __device__ __attribute__((aligned(256))) uint4 h_sink[64];
@@ -177,7 +171,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const int row = (wave * NBI + i) * 16 + lrow;  // = tap * BN + nn
     const int piece = lpc ^ (((row >> 2) & 1) << 1);
     const int tap = row / BN, nn = row - (row / BN) * BN;
-    boff[i] = row < KT * BN ? (unsigned)((hperm(nn) * K + tap * p.cin + piece * 8) * 2) : OOB;
+    boff[i] = row < KT * BN ? (unsigned)((pair_perm(nn) * K + tap * p.cin + piece * 8) * 2) : OOB;
   }
   uintptr_t pbase = 0, bbase = 0;
   char* iPs = smem;

@@ -55,6 +55,15 @@ __device__ __forceinline__ float border_corr(const float* __restrict__ U, int oh
   return c;
 }
 
+// Column permutation inside each 32-column pair of 16x16x32 MFMA fragments: when LDS
+// weight row nn holds GEMM column pair_perm(nn) and the MFMA runs with the operands
+// swapped (C^T = W^T A^T), lane group g (= lane >> 4) of fragments (2p, 2p+1) holds the
+// 8 CONSECUTIVE columns 32p + 8g .. +7 of its pixel (4 per fragment): one 16-byte
+// store per (pixel, 8 columns) straight from the accumulators.
+__host__ __device__ constexpr int pair_perm(int nn) {
+  return 32 * (nn >> 5) + 8 * ((nn & 15) >> 2) + 4 * ((nn >> 4) & 1) + (nn & 3);
+}
+
 template <typename T> struct Mma;
 template <> struct Mma<bf16> {
   static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {

@@ -68,12 +68,13 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   const int gidx = xcd * p.gpx + grp, ngrp = 8 * p.gpx;
   const long per = (p.tiles + ngrp - 1) / ngrp;
   const long t0 = gidx * per, t1 = t0 + per < p.tiles ? t0 + per : p.tiles;
-  // the weight block, once
+  // the weight block, once; LDS row nn holds block column pair_perm(nn), so a lane's
+  // fragment pair (2q, 2q+1) ends up with 8 consecutive columns (16-byte stores)
   const int pieces = K / 8;
   for (int q = tid; q < BN * pieces; q += NW * 64) {
     const int row = q / pieces, pc = q - row * pieces;
     *reinterpret_cast<uint4*>(smem + row * ldsrow + pc * 16) =
-        *reinterpret_cast<const uint4*>(p.b + (size_t)(nb * BN + row) * K + pc * 8);
+        *reinterpret_cast<const uint4*>(p.b + (size_t)(nb * BN + pair_perm(row)) * K + pc * 8);
   }
   __syncthreads();
 
@@ -144,53 +145,57 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
         compute(ks + 2, A2);
       }
     }
-    // epilogue from registers
-    float s1[MODE == 0 ? FN : 1][4], s2[MODE == 0 ? FN : 1][4];
+    // epilogue from registers: fragment pair (2q, 2q+1) gives the lane 8 consecutive
+    // columns n .. n+7 of its pixel (pair_perm) -> one 16-byte store per (pixel, pair)
+    // (8-byte stores, one per fragment, took 40 % of up8's forward: store-issue-bound)
+    constexpr int FP = FN / 2;
+    float s1[MODE == 0 ? FP : 1][8], s2[MODE == 0 ? FP : 1][8];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = nb * BN + j * 16 + kq * 4;  // first of the lane's 4 columns
+    for (int q = 0; q < FP; ++q) {
+      const int n = nb * BN + q * 32 + kq * 8;  // first of the lane's 8 columns (8 | cout)
       if constexpr (MODE == 0) {
         const int tap = n / p.cout, co = n - tap * p.cout;
-        const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + ((p.flags & CNNITMO_BIAS_PER_COL) ? n : co))
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 sc4 = aff ? *reinterpret_cast<const float4*>(p.aff_scale + co) : make_float4(1.f, 1.f, 1.f, 1.f);
-        const float4 sh4 = aff ? *reinterpret_cast<const float4*>(p.aff_shift + co) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float bj[4] = {b4.x, b4.y, b4.z, b4.w}, sj[4] = {sc4.x, sc4.y, sc4.z, sc4.w},
-                    hj[4] = {sh4.x, sh4.y, sh4.z, sh4.w};
+        float bj[8], sj[8], hj[8];
+        if (p.bias) Pack16<float>::load(p.bias + ((p.flags & CNNITMO_BIAS_PER_COL) ? n : co), bj),
+            Pack16<float>::load(p.bias + ((p.flags & CNNITMO_BIAS_PER_COL) ? n : co) + 4, bj + 4);
+        else
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+          for (int k = 0; k < 8; ++k) bj[k] = 0.f;
+        if (aff) {
+          Pack16<float>::load(p.aff_scale + co, sj);
+          Pack16<float>::load(p.aff_scale + co + 4, sj + 4);
+          Pack16<float>::load(p.aff_shift + co, hj);
+          Pack16<float>::load(p.aff_shift + co + 4, hj + 4);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s1[q][k] = s2[q][k] = 0.f;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const bool ok = px[f] < P;
-          bf16 o[4];
+          float v[8];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[f][j][r] + bj[r];
-            if (relu) v = fmaxf(v, 0.f);
-            if (aff) v = v * sj[r] + hj[r];
-            const float vs = ok ? v : 0.f;
-            s1[j][r] += vs;
-            s2[j][r] += vs * vs;
-            o[r] = from_f32<bf16>(v);
+          for (int k = 0; k < 8; ++k) {
+            v[k] = acc[f][2 * q + (k >> 2)][k & 3] + bj[k];
+            if (relu) v[k] = fmaxf(v[k], 0.f);
+            if (aff) v[k] = v[k] * sj[k] + hj[k];
+            const float vs = ok ? v[k] : 0.f;
+            s1[q][k] += vs;
+            s2[q][k] += vs * vs;
           }
           if (ok) {
             const int pi = (int)px[f], img = pi / hw, rem = pi - img * hw, y = rem / p.w, x = rem - y * p.w;
             const size_t op = ((size_t)img * 2 * p.h + 2 * y + (tap >> 1)) * 2 * p.w + 2 * x + (tap & 1);
-            u32x2 pk;
-            __builtin_memcpy(&pk, o, 8);
-            *reinterpret_cast<u32x2*>(p.out + op * p.out_ld + p.out_off + co) = pk;
+            Pack16<bf16>::store(p.out + op * p.out_ld + p.out_off + co, v);
           }
         }
       } else {
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           if (px[f] < P) {
-            bf16 o[4];
+            float v[8];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = from_f32<bf16>(acc[f][j][r]);
-            u32x2 pk;
-            __builtin_memcpy(&pk, o, 8);
-            *reinterpret_cast<u32x2*>(p.out + (size_t)px[f] * p.out_ld + p.out_off + n) = pk;
+            for (int k = 0; k < 8; ++k) v[k] = acc[f][2 * q + (k >> 2)][k & 3];
+            Pack16<bf16>::store(p.out + (size_t)px[f] * p.out_ld + p.out_off + n, v);
           }
         }
       }
@@ -198,12 +203,12 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
     if constexpr (MODE == 0) {
       if (stats) {
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+        for (int q = 0; q < FP; ++q)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float a1 = row16_sum(s1[j][r]), a2 = row16_sum(s2[j][r]);
+          for (int k = 0; k < 8; ++k) {
+            const float a1 = row16_sum(s1[q][k]), a2 = row16_sum(s2[q][k]);
             if (frow == 0) {
-              const int c = j * 16 + kq * 4 + r;
+              const int c = q * 32 + kq * 8 + k;
               sl[c * 2] += a1;
               sl[c * 2 + 1] += a2;
             }
