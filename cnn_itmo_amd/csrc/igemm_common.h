@@ -96,7 +96,7 @@ long halo_stat_rows(const FwdArgs& a);
 // tconv_stream.hip: Conv2DTranspose fwd (mode 0) / input-gradient (mode 1) as a
 // streamed GEMM with the weight block resident in LDS (bf16)
 bool tconv_stream_handles(int mode, int h, int w, int cin, int cout, bool epi);
-long tconv_stream_rows(int n, int h, int w);
+long tconv_stream_rows(int mode, int n, int h, int w, int cin, int cout, bool epi);
 const char* tconv_stream_name(int mode, int h, int w, int cin, int cout, bool epi);
 int launch_tconv_stream(int mode, const void* a, long a_ld, int a_off, const void* b, int n, int h, int w,
                         int cin, int cout, void* out, long out_ld, int out_off, const float* bias, int flags,

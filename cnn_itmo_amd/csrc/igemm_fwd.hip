@@ -337,7 +337,8 @@ extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int ci
 }
 
 extern "C" long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int cin, int cout) {
-  if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false)) return tconv_stream_rows(n, h, w);
+  if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false))
+    return tconv_stream_rows(0, n, h, w, cin, cout, false);
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout)) return tconv_ws_rows(cin, cout);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
@@ -543,7 +544,7 @@ extern "C" int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h,
 
 extern "C" long cnnitmo_tconv2x2_dgrad_bn_rows(int dtype, int n, int h, int w, int cout, int cin) {
   if (dtype != CNNITMO_BF16 || !tconv_stream_handles(1, h, w, cin, cout, true)) return 0;
-  return tconv_stream_rows(n, h, w);
+  return tconv_stream_rows(1, n, h, w, cin, cout, true);
 }
 
 // Name of the kernel cnnitmo_tconv2x2_dgrad_bn launches for these sizes (for profiles).

@@ -7,9 +7,10 @@
 //   * the activations stream through an LDS-DMA ring (64-pixel tiles x 128-deep
 //     K chunks, 16 KB per stage), each byte read from HBM once per column block,
 //   * the MFMA runs with the operands swapped (C^T = W^T A^T), so a lane ends up
-//     with 4 consecutive output channels of one pixel and stores them straight
-//     from registers (8-byte buffer stores, out-of-range pixels dropped by the
-//     range check): no LDS staging, no barrier in the epilogue.
+//     with output channels of one pixel and stores them straight from registers
+//     (the weight rows in pair_perm order: 8 consecutive channels, one 16-byte
+//     buffer store; out-of-range pixels dropped by the range check): no LDS
+//     staging, no barrier in the epilogue.
 // MODE 0 (forward): A = x [P][cin] (a row per input pixel), B = k [4*cout][cin];
 //   GEMM column n = tap*cout + co is scattered to output pixel (2y+a, 2x+b).
 //   Epilogue: bias (per column), ReLU, inference affine, BN partial sums.
@@ -65,7 +66,7 @@ struct TSArgs {
   int flags;
   const float* aff_scale;
   const float* aff_shift;
-  float* stats;  // MODE 0: [ntiles*2][2][N]; MODE 1 EPI: [ntiles*2][N] sums of dz
+  float* stats;  // MODE 0: [ntiles*WM][2][N]; MODE 1 EPI: [ntiles*WM][N] sums of dz
   const float* coef;  // MODE 1 EPI: [3][N]
   const bf16* r;
   long r_ld;
@@ -74,8 +75,11 @@ struct TSArgs {
 
 template <int MODE, int BN, int ST, bool EPI>
 struct TSCfg {
-  static constexpr int NT = 512, BM = 64, KC = 128;  // 8 waves: 2 (pixels) x 4 (columns)
-  static constexpr int FM = 2, FN = BN / 64;          // wave tile 32 px x BN/4 columns
+  static constexpr int NT = 512, BM = 64, KC = 128;
+  // 8 waves: WM (pixels) x WN (columns), every wave owning >= 32 columns (a pair of
+  // fragments, for the 16-byte stores): BN 256/128: 2 x 4, BN 64: 4 x 2
+  static constexpr int WN = BN >= 128 ? 4 : BN / 32, WM = 8 / WN;
+  static constexpr int FM = BM / 16 / WM, FN = BN / WN / 16;  // wave tile 16*FM px x 16*FN columns
   static constexpr int STAGE = BM * KC * 2;           // 16 KB
   static constexpr int RSLOT = EPI ? BM * BN * 2 : 0;
   static constexpr int PAR = 3 * BN * 4;
@@ -97,7 +101,8 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
+  constexpr int WN = C::WN;
+  const int wm = wave / WN, wn = wave % WN;  // (rows of the stats / sums: WM per tile)
   // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (b % 8); the
   // column blocks of one tile range live on the SAME XCD, so the re-reads of an
   // A tile by the other column blocks hit that XCD's L2
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
     const i32x4 rs = dma::rsrc((uintptr_t)(p.b + (size_t)n0 * K));
     for (int q = wave; q < rows / 16; q += 8) {
       const int row = q * 16 + (lane >> 2), piece = (lane & 3) ^ (((row >> 2) & 1) << 1);
-      const int ks = row / BN, n = row - ks * BN;
+      const int ks = row / BN, n = pair_perm(row - ks * BN);  // (16-byte stores: see the epilogue)
       dma::lds16((unsigned)((n * K + ks * 32 + piece * 8) * 2), rs, Bres + q * 1024);
     }
     for (int c = tid; c < BN; c += C::NT) {
@@ -214,11 +219,11 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
       uint4 af[FM], bfr[FN];
 #pragma unroll
       for (int f = 0; f < FM; ++f)
-        af[f] = *reinterpret_cast<const uint4*>(S + rsw(ks * 64 + wm * 32 + f * 16 + (lane & 15), lane >> 4));
+        af[f] = *reinterpret_cast<const uint4*>(S + rsw(ks * 64 + wm * (16 * FM) + f * 16 + (lane & 15), lane >> 4));
 #pragma unroll
       for (int j = 0; j < FN; ++j)
         bfr[j] = *reinterpret_cast<const uint4*>(
-            Bres + rsw((kc * 4 + ks) * BN + wn * (BN / 4) + j * 16 + (lane & 15), lane >> 4));
+            Bres + rsw((kc * 4 + ks) * BN + wn * (BN / WN) + j * 16 + (lane & 15), lane >> 4));
 #pragma unroll
       for (int f = 0; f < FM; ++f)
 #pragma unroll
@@ -227,116 +232,123 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   };
 
   const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE, stats = p.flags & CNNITMO_STATS;
-  // stores per tile epilogue (all issued, out-of-range ones dropped): FM*FN outputs
-  // + MODE 0 stats 2*FN (lanes 0/16/32/48) + EPI sums FN
-  constexpr int SOUT = FM * FN;
-  const int S = SOUT + (MODE == 0 ? (stats ? 2 * FN : 0) : (EPI ? FN : 0));
+  // Epilogue straight from the accumulators.  The resident weight rows are in pair_perm
+  // order, so fragments (2jp, 2jp+1) give a lane 8 CONSECUTIVE columns c .. c+7 of its
+  // pixel: one 16-byte store per (pixel, pair).
+  // stores per tile epilogue (all issued, out-of-range ones dropped): FM*FP outputs
+  // + MODE 0 stats 4*FP (lanes 0/16/32/48) + EPI sums 2*FP
+  constexpr int FP = FN / 2;
+  static_assert(FN % 2 == 0, "column pairs");
+  constexpr int SOUT = FM * FP;
+  const int S = SOUT + (MODE == 0 ? (stats ? 4 * FP : 0) : (EPI ? 2 * FP : 0));
+  typedef float f32x8_ __attribute__((ext_vector_type(8)));
   auto epilogue = [&](long t, int rslot) {
     int img, y, x0;
     tile_pos(t, img, y, x0);
-    float s1[FN][4], s2[FN][4];
+    float s1[FP][8], s2[FP][8];
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FP; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) s1[j][r] = s2[j][r] = 0.f;
+      for (int k = 0; k < 8; ++k) s1[j][k] = s2[j][k] = 0.f;
     if constexpr (MODE == 0) {
       const __amdgpu_buffer_rsrc_t os =
           srsrc(p.out + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.out_ld + p.out_off);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = wn * (BN / 4) + j * 16 + (lane >> 4) * 4;  // first of this lane's 4 columns
-        const int n = n0 + c, tap = n / p.cout, co = n - tap * p.cout;
-        const f32x4_ bj = *reinterpret_cast<const f32x4_*>(par + c);
-        const f32x4_ sj = *reinterpret_cast<const f32x4_*>(par + BN + c);
-        const f32x4_ hj = *reinterpret_cast<const f32x4_*>(par + 2 * BN + c);
+      for (int jp = 0; jp < FP; ++jp) {
+        const int c = wn * (BN / WN) + jp * 32 + (lane >> 4) * 8;  // first of this lane's 8 columns
+        const int n = n0 + c, tap = n / p.cout, co = n - tap * p.cout;  // (8 | cout: one tap)
+        const f32x8_ bj = *reinterpret_cast<const f32x8_*>(par + c);
+        const f32x8_ sj = *reinterpret_cast<const f32x8_*>(par + BN + c);
+        const f32x8_ hj = *reinterpret_cast<const f32x8_*>(par + 2 * BN + c);
 #pragma unroll
         for (int f = 0; f < FM; ++f) {
-          const int px = wm * 32 + f * 16 + (lane & 15);
+          const int px = wm * (16 * FM) + f * 16 + (lane & 15);
           const bool ok = x0 + px < p.w;
-          bf16 o[4];
+          bf16x8 o;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[f][j][r] + bj[r];
+          for (int k = 0; k < 8; ++k) {
+            float v = acc[f][2 * jp + (k >> 2)][k & 3] + bj[k];
             if (relu) v = fmaxf(v, 0.f);
-            if (aff) v = v * sj[r] + hj[r];
+            if (aff) v = v * sj[k] + hj[k];
             const float vs = ok ? v : 0.f;
-            s1[j][r] += vs;
-            s2[j][r] += vs * vs;
-            o[r] = from_f32<bf16>(v);
+            s1[jp][k] += vs;
+            s2[jp][k] += vs * vs;
+            o[k] = from_f32<bf16>(v);
           }
-          u32x2 pk;
-          __builtin_memcpy(&pk, o, 8);
           const unsigned off = (unsigned)((((tap >> 1) * W2 + 2 * px + (tap & 1)) * p.out_ld + co) * 2);
-          __builtin_amdgcn_raw_buffer_store_b64(pk, os, ok ? off : OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), os, ok ? off : OOB, 0, 0);
         }
       }
       if (stats) {
-        const long row = (t * 2 + wm);
+        const long row = (t * C::WM + wm);
         const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)row * 2 * p.N);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
+        for (int jp = 0; jp < FP; ++jp) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            s1[j][r] = row16_sum(s1[j][r]);
-            s2[j][r] = row16_sum(s2[j][r]);
+          for (int k = 0; k < 8; ++k) {
+            s1[jp][k] = row16_sum(s1[jp][k]);
+            s2[jp][k] = row16_sum(s2[jp][k]);
           }
-          const int n = n0 + wn * (BN / 4) + j * 16 + (lane >> 4) * 4;
-          const f32x4_ a1 = {s1[j][0], s1[j][1], s1[j][2], s1[j][3]};
-          const f32x4_ a2 = {s2[j][0], s2[j][1], s2[j][2], s2[j][3]};
+          const int n = n0 + wn * (BN / WN) + jp * 32 + (lane >> 4) * 8;
           const bool w0 = (lane & 15) == 0;
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss, w0 ? (unsigned)(n * 4) : OOB, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a2), ss,
-                                                 w0 ? (unsigned)((p.N + n) * 4) : OOB, 0, 0);
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f32x4_ a1 = {s1[jp][4 * h], s1[jp][4 * h + 1], s1[jp][4 * h + 2], s1[jp][4 * h + 3]};
+            const f32x4_ a2 = {s2[jp][4 * h], s2[jp][4 * h + 1], s2[jp][4 * h + 2], s2[jp][4 * h + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss,
+                                                   w0 ? (unsigned)((n + 4 * h) * 4) : OOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a2), ss,
+                                                   w0 ? (unsigned)((p.N + n + 4 * h) * 4) : OOB, 0, 0);
+          }
         }
       }
     } else {
       const __amdgpu_buffer_rsrc_t os = srsrc(p.out + (((size_t)img * p.h + y) * p.w + x0) * p.out_ld + p.out_off);
       const char* R = rr + rslot * C::RSLOT;
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int c = wn * (BN / 4) + j * 16 + (lane >> 4) * 4;
-        f32x4_ ca = {}, cb = {}, ce = {};
+      for (int jp = 0; jp < FP; ++jp) {
+        const int c = wn * (BN / WN) + jp * 32 + (lane >> 4) * 8;
+        f32x8_ ca = {}, cb = {}, ce = {};
         if constexpr (EPI) {
-          ca = *reinterpret_cast<const f32x4_*>(par + c);
-          cb = *reinterpret_cast<const f32x4_*>(par + BN + c);
-          ce = *reinterpret_cast<const f32x4_*>(par + 2 * BN + c);
+          ca = *reinterpret_cast<const f32x8_*>(par + c);
+          cb = *reinterpret_cast<const f32x8_*>(par + BN + c);
+          ce = *reinterpret_cast<const f32x8_*>(par + 2 * BN + c);
         }
 #pragma unroll
         for (int f = 0; f < FM; ++f) {
-          const int px = wm * 32 + f * 16 + (lane & 15);
+          const int px = wm * (16 * FM) + f * 16 + (lane & 15);
           const bool ok = x0 + px < p.w;
-          bf16 o[4];
+          bf16x8 o;
           if constexpr (EPI) {
-            // r[px][c..c+3]: piece c/8 of row px, stored at piece (c/8) ^ (px & (PPR-1))
-            const bf16* rv = reinterpret_cast<const bf16*>(
-                R + (px * PPR + ((c >> 3) ^ (px & (PPR - 1)))) * 16 + (c & 7) * 2);
-            const uint2 r4 = *reinterpret_cast<const uint2*>(rv);
-            const bf16* rq = reinterpret_cast<const bf16*>(&r4);
+            // r[px][c..c+7]: piece c/8 of row px, stored at piece (c/8) ^ (px & (PPR-1))
+            const bf16x8 rq = *reinterpret_cast<const bf16x8*>(R + (px * PPR + ((c >> 3) ^ (px & (PPR - 1)))) * 16);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float gg = to_f32(from_f32<bf16>(acc[f][j][r])), rvv = to_f32(rq[r]);
-              o[r] = from_f32<bf16>(rvv > 0.f ? ca[r] * gg - cb[r] * rvv + ce[r] : 0.f);
-              s1[j][r] += ok ? to_f32(o[r]) : 0.f;
+            for (int k = 0; k < 8; ++k) {
+              const float gg = to_f32(from_f32<bf16>(acc[f][2 * jp + (k >> 2)][k & 3])), rvv = to_f32(rq[k]);
+              o[k] = from_f32<bf16>(rvv > 0.f ? ca[k] * gg - cb[k] * rvv + ce[k] : 0.f);
+              s1[jp][k] += ok ? to_f32(o[k]) : 0.f;
             }
           } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = from_f32<bf16>(acc[f][j][r]);
+            for (int k = 0; k < 8; ++k) o[k] = from_f32<bf16>(acc[f][2 * jp + (k >> 2)][k & 3]);
           }
-          u32x2 pk;
-          __builtin_memcpy(&pk, o, 8);
-          __builtin_amdgcn_raw_buffer_store_b64(pk, os, ok ? (unsigned)((px * p.out_ld + n0 + c) * 2) : OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), os,
+                                                 ok ? (unsigned)((px * p.out_ld + n0 + c) * 2) : OOB, 0, 0);
         }
       }
       if constexpr (EPI) {
-        const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)(t * 2 + wm) * p.N);
+        const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)(t * C::WM + wm) * p.N);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
+        for (int jp = 0; jp < FP; ++jp) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) s1[j][r] = row16_sum(s1[j][r]);
-          const int n = n0 + wn * (BN / 4) + j * 16 + (lane >> 4) * 4;
-          const f32x4_ a1 = {s1[j][0], s1[j][1], s1[j][2], s1[j][3]};
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss,
-                                                 (lane & 15) == 0 ? (unsigned)(n * 4) : OOB, 0, 0);
+          for (int k = 0; k < 8; ++k) s1[jp][k] = row16_sum(s1[jp][k]);
+          const int n = n0 + wn * (BN / WN) + jp * 32 + (lane >> 4) * 8;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f32x4_ a1 = {s1[jp][4 * h], s1[jp][4 * h + 1], s1[jp][4 * h + 2], s1[jp][4 * h + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss,
+                                                   (lane & 15) == 0 ? (unsigned)((n + 4 * h) * 4) : OOB, 0, 0);
+          }
         }
       }
     }
@@ -437,7 +449,12 @@ bool tconv_stream_handles(int mode, int h, int w, int cin, int cout, bool epi) {
   return ts_plan(mode, h, w, cin, cout, epi, pl);
 }
 
-long tconv_stream_rows(int n, int h, int w) { return (long)n * h * ((w + 63) / 64) * 2; }
+long tconv_stream_rows(int mode, int n, int h, int w, int cin, int cout, bool epi) {
+  TSPlan pl;
+  if (!ts_plan(mode, h, w, cin, cout, epi, pl)) return 0;
+  const int wm = pl.bn >= 128 ? 2 : 8 / (pl.bn / 32);  // TSCfg::WM: one row per pixel wave-row
+  return (long)n * h * ((w + 63) / 64) * wm;
+}
 
 const char* tconv_stream_name(int mode, int h, int w, int cin, int cout, bool epi) {
   TSPlan pl;
