@@ -896,6 +896,252 @@ __global__ void head_kernel(const T* __restrict__ x, int N, int H, int Hv, int W
   }
 }
 
+// The same head, one wave per 64 consecutive pixels per iteration, in two layouts:
+//   * channel layout (loads, dot products, dW, dx): LPP = cin/VE lanes per pixel, each
+//     lane issuing LPP 16-byte loads up front (pixel u*64/LPP + lane/LPP): 1 KB per
+//     instruction, LPP KB in flight per wave; the dot products reduced over the LPP
+//     lanes with DPP (quad_perm xor 1/2, half-row and row mirrors: VALU, no LDS);
+//   * pixel layout (sigmoid, loss, accuracy, dz, target and g3/yhat): lane = pixel,
+//     the per-pixel math done once (head_kernel did it on all LPP lanes of a pixel),
+//     target / g3 / yhat as 12-byte runs of consecutive lanes.
+// z and dz cross between the two through a 1 KB LDS slice per wave (no barrier: one
+// wave owns the slice, LDS executes a wave's instructions in order).  Bench shape
+// (32 x 1088 x 1920 x 64 bf16, g3 out; tools/probe_elem.py): head_kernel 4.85 ms
+// (2.1 TB/s), head2_kernel 2.35 ms (4.3 TB/s; a torch copy of x runs at 4.9 TB/s).
+template <int LPP>
+__device__ __forceinline__ float lane_group_sum(float v) {
+  if constexpr (LPP >= 2) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+  if constexpr (LPP >= 4) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+  if constexpr (LPP >= 8) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+  if constexpr (LPP >= 16) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ void unpack16(const uint4& q, float* v) {
+  if constexpr (Vec16<T>::N == 8) {
+    const bf16x8 b = __builtin_bit_cast(bf16x8, q);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)b[i];
+  } else {
+    v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+  }
+}
+
+// BWD: loss + gradients; G3: the gradient leaves as g3 [P][3] (else dx = dz . W)
+template <typename T, int LPP, bool BWD, bool G3>
+__global__ __launch_bounds__(256) void head2_kernel(const T* __restrict__ x, int H, int Hv, int W, long P,
+                                                    const float* __restrict__ wt, const float* __restrict__ bias,
+                                                    const float* __restrict__ target, float* __restrict__ yhat,
+                                                    T* __restrict__ dx, float inv_numel, float* __restrict__ part,
+                                                    const float* __restrict__ fs, const float* __restrict__ fh,
+                                                    float* __restrict__ g3) {
+  constexpr int VE = Vec16<T>::N, CIN = LPP * VE, PPI = 64 / LPP;  // pixels per load instruction
+  __shared__ float4 zs[4][64];
+  __shared__ float red[4][3 * CIN + 5];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane % LPP, c0 = sub * VE, pq = lane / LPP;
+  float w[3][VE], wf[3][VE], bf[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+#pragma unroll
+    for (int e = 0; e < VE; ++e) {
+      w[o][e] = BWD && !G3 ? wt[o * CIN + c0 + e] : 0.f;  // (dx only)
+      const float wo = wt[o * CIN + c0 + e];
+      wf[o][e] = fs ? wo * fs[c0 + e] : wo;
+      if (fh) bf[o] += wo * fh[c0 + e];
+    }
+    bf[o] = lane_group_sum<LPP>(bf[o]);
+  }
+  const float b0 = bias[0] + bf[0], b1 = bias[1] + bf[1], b2 = bias[2] + bf[2];
+  float dwacc[3][VE];
+#pragma unroll
+  for (int o = 0; o < 3; ++o)
+#pragma unroll
+    for (int e = 0; e < VE; ++e) dwacc[o][e] = 0.f;
+  float lsum = 0.f, corr = 0.f, db0 = 0.f, db1 = 0.f, db2 = 0.f;
+  const int hw = H * W;
+  const long ngroups = (P + 63) / 64, nw = (long)gridDim.x * 4;
+  // a group's x (channel layout) and target (pixel layout) loads, all issued first and
+  // branch-free (buffer loads, out-of-range ones read 0).  (Issuing the next group's
+  // loads before this group's math measured no faster: 2.35 vs 2.35 ms at the bench
+  // shape, where a torch copy of the same bytes runs at 4.9 TB/s.)
+  const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(BWD ? target : nullptr), (short)0, BWD ? (int)(P / hw * Hv * W * 12) : 0, 0x00020000);
+  auto fetch = [&](long g, uint4 (&xq)[LPP], float (&tq)[3]) {
+    const long b = g * 64;
+    const long np_ = P - b < 64 ? (P - b > 0 ? P - b : 0) : 64;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(x + (b < P ? b : 0) * CIN), (short)0, (int)np_ * CIN * (int)sizeof(T), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < LPP; ++u)
+      xq[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            xr, (unsigned)(((u * PPI + pq) * CIN + c0) * sizeof(T)), 0, 0));
+    if constexpr (BWD) {
+      const int pp = (int)b + lane;
+      const bool ok = lane < np_;
+      const int n = ok ? pp / hw : 0, rem = ok ? pp - n * hw : 0, h = rem / W, wc = rem - h * W;
+      const unsigned off = ok && h < Hv ? (((unsigned)n * Hv + h) * W + wc) * 12u : 0x80000000u;
+#pragma unroll
+      for (int o = 0; o < 3; ++o) tq[o] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(tr, off + 4 * o, 0, 0));
+    }
+  };
+  uint4 xv[LPP];
+  float tv[3] = {0.f, 0.f, 0.f};
+  for (long grp = (long)blockIdx.x * 4 + wave; grp < ngroups; grp += nw) {
+    fetch(grp, xv, tv);
+    const long base = grp * 64;
+    const int np = (int)(P - base < 64 ? P - base : 64);
+    // pixel layout (32-bit index math: P < 2^31, checked by the launchers)
+    const int p = (int)base + lane;
+    const bool inb = lane < np;
+    const int n = inb ? p / hw : 0, rem = inb ? p - n * hw : 0, h = rem / W, wc = rem - h * W;
+    const bool valid = inb && h < Hv;
+    const size_t tix = (((size_t)n * Hv + h) * W + wc) * 3;
+    const float t0 = tv[0], t1 = tv[1], t2 = tv[2];
+#pragma unroll
+    for (int u = 0; u < LPP; ++u) {
+      float v[VE];
+      unpack16<T>(xv[u], v);
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        s0 += v[e] * wf[0][e];
+        s1 += v[e] * wf[1][e];
+        s2 += v[e] * wf[2][e];
+      }
+      s0 = lane_group_sum<LPP>(s0);
+      s1 = lane_group_sum<LPP>(s1);
+      s2 = lane_group_sum<LPP>(s2);
+      if (sub == 0) zs[wave][u * PPI + pq] = make_float4(s0, s1, s2, 0.f);
+    }
+    __builtin_amdgcn_wave_barrier();
+    const float4 z = zs[wave][lane];
+    const float y0 = 1.f / (1.f + expf(-(z.x + b0)));
+    const float y1 = 1.f / (1.f + expf(-(z.y + b1)));
+    const float y2 = 1.f / (1.f + expf(-(z.z + b2)));
+    if (!BWD) {
+      if (valid) {
+        yhat[tix] = y0;
+        yhat[tix + 1] = y1;
+        yhat[tix + 2] = y2;
+      }
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    if (valid) {
+      const float e0 = y0 - t0, e1 = y1 - t1, e2 = y2 - t2;
+      lsum += e0 * e0 + e1 * e1 + e2 * e2;
+      const int at = (t1 > t0) ? ((t2 > t1) ? 2 : 1) : ((t2 > t0) ? 2 : 0);
+      const int ap = (y1 > y0) ? ((y2 > y1) ? 2 : 1) : ((y2 > y0) ? 2 : 0);
+      corr += (at == ap) ? 1.f : 0.f;
+      d0 = 2.f * e0 * y0 * (1.f - y0) * inv_numel;
+      d1 = 2.f * e1 * y1 * (1.f - y1) * inv_numel;
+      d2 = 2.f * e2 * y2 * (1.f - y2) * inv_numel;
+    }
+    db0 += d0;
+    db1 += d1;
+    db2 += d2;
+    if (G3 && inb) {
+      g3[(size_t)p * 3] = d0;
+      g3[(size_t)p * 3 + 1] = d1;
+      g3[(size_t)p * 3 + 2] = d2;
+    }
+    zs[wave][lane] = make_float4(d0, d1, d2, 0.f);
+    __builtin_amdgcn_wave_barrier();
+    // back to the channel layout: dW (and dx = dz . W without g3)
+#pragma unroll
+    for (int u = 0; u < LPP; ++u) {
+      const float4 d = zs[wave][u * PPI + pq];
+      float v[VE];
+      asm volatile("" : "+v"(xv[u].x), "+v"(xv[u].y), "+v"(xv[u].z), "+v"(xv[u].w));  // unpack again: keeping all LPP*VE floats live costs occupancy
+      unpack16<T>(xv[u], v);
+#pragma unroll
+      for (int e = 0; e < VE; ++e) {
+        dwacc[0][e] += d.x * v[e];
+        dwacc[1][e] += d.y * v[e];
+        dwacc[2][e] += d.z * v[e];
+      }
+      if (!G3 && u * PPI + pq < np) {
+        float g[VE];
+#pragma unroll
+        for (int e = 0; e < VE; ++e) g[e] = d.x * w[0][e] + d.y * w[1][e] + d.z * w[2][e];
+        Pack16<T>::store(dx + (size_t)(base + u * PPI + pq) * CIN + c0, g);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!BWD) return;
+  // reduce: dW over the lanes of equal `sub`, the scalars over the wave, then the 4 waves
+#pragma unroll
+  for (int o = 0; o < 3; ++o)
+#pragma unroll
+    for (int e = 0; e < VE; ++e)
+#pragma unroll
+      for (int m = LPP; m < 64; m <<= 1) dwacc[o][e] += __shfl_xor(dwacc[o][e], m, 64);
+  lsum = wave_sum(lsum);
+  corr = wave_sum(corr);
+  db0 = wave_sum(db0);
+  db1 = wave_sum(db1);
+  db2 = wave_sum(db2);
+  if (lane < LPP) {
+#pragma unroll
+    for (int o = 0; o < 3; ++o)
+#pragma unroll
+      for (int e = 0; e < VE; ++e) red[wave][5 + o * CIN + c0 + e] = dwacc[o][e];
+  }
+  if (lane == 0) {
+    red[wave][0] = lsum;
+    red[wave][1] = corr;
+    red[wave][2] = db0;
+    red[wave][3] = db1;
+    red[wave][4] = db2;
+  }
+  __syncthreads();
+  float* out = part + (size_t)blockIdx.x * (5 + 3 * CIN);
+  for (int k = tid; k < 5 + 3 * CIN; k += 256) out[k] = red[0][k] + red[1][k] + red[2][k] + red[3][k];
+}
+
+// head2_kernel for this dtype / width, or false (head_kernel then)
+template <bool BWD>
+static bool launch_head2(int dtype, const void* x, int n, int h, int h_valid, int w, int cin, const float* wt,
+                         const float* b, const float* target, float* yhat, void* dx, float inv_numel,
+                         float* part, const float* scale, const float* shift, float* g3, int G_, hipStream_t s) {
+  static const bool en = [] {  // CNNITMO_HEAD2=0: head_kernel (A/B)
+    const char* e = getenv("CNNITMO_HEAD2");
+    return !e || atoi(e) != 0;
+  }();
+  const long P = (long)n * h * w;
+  const int lpp = cin / (dtype == CNNITMO_BF16 ? 8 : 4);
+  // 32-bit pixel and target-byte offsets inside the kernel
+  if (!en || P >= (1L << 30) || (long)n * h_valid * w * 12 >= (1L << 31)) return false;
+#define H2K(T, L, G)                                                                                          \
+  hipLaunchKernelGGL((head2_kernel<T, L, BWD, G>), dim3(G_), dim3(256), 0, s, (const T*)x, h, h_valid, w, P, wt, \
+                     b, target, yhat, (T*)dx, inv_numel, part, scale, shift, g3)
+#define H2(T, L)                  \
+  do {                            \
+    if (BWD && g3) H2K(T, L, BWD); \
+    else H2K(T, L, false);        \
+  } while (0)
+#define H2L(T)                     \
+  switch (lpp) {                   \
+    case 2: H2(T, 2); return true;   \
+    case 4: H2(T, 4); return true;   \
+    case 8: H2(T, 8); return true;   \
+    case 16: H2(T, 16); return true; \
+    default: return false;           \
+  }
+  if (dtype == CNNITMO_BF16) {
+    H2L(bf16)
+  } else {
+    H2L(float)
+  }
+#undef H2L
+#undef H2
+#undef H2K
+}
+
 extern "C" int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
                                 const float* wt, const float* b, const float* scale,
                                 const float* shift, float* yhat, void* stream) {
@@ -906,6 +1152,9 @@ extern "C" int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_va
   const long P = (long)n * h * w;
   CNN_REQUIRE(P < (1L << 31), "head: too many pixels");
   const int G = cnnitmo_head_rows(P);
+  if (launch_head2<false>(dtype, x, n, h, h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale,
+                          shift, nullptr, G, s))
+    return cnnitmo_check_launch("head_fwd");
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL((head_kernel<bf16, false>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
                        h_valid, w, cin, wt, b, nullptr, yhat, nullptr, 0.f, nullptr, scale, shift, nullptr);
@@ -926,6 +1175,9 @@ static int head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int
   CNN_REQUIRE(P < (1L << 31), "head: too many pixels");
   const int G = cnnitmo_head_rows(P);
   const float inv_numel = (float)(1.0 / ((double)n * h_valid * w * 3));
+  if (launch_head2<true>(dtype, x, n, h, h_valid, w, cin, wt, b, target, nullptr, dx, inv_numel, part, scale,
+                         shift, g3, G, s))
+    return cnnitmo_check_launch("head_fwd_bwd");
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL((head_kernel<bf16, true>), dim3(G), dim3(256), 0, s, (const bf16*)x, n, h,
                        h_valid, w, cin, wt, b, target, nullptr, (bf16*)dx, inv_numel, part, scale, shift, g3);

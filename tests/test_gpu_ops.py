@@ -344,10 +344,15 @@ def test_bn_train_fwd_bwd(dt, drop):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-def test_head(dt):
+@pytest.mark.parametrize("C,H,W", [(64, 8, 16),
+                                   # head2_kernel at 2..16 lanes per pixel, ragged 64-pixel groups
+                                   (16, 5, 13), (32, 9, 31), (128, 6, 11),
+                                   # head_kernel (32 / 64 lanes per pixel)
+                                   (256, 4, 9)])
+def test_head(dt, C, H, W):
     from cnn_itmo_amd import ops
-    rng = np.random.default_rng(6)
-    N, Hv, H, W, C = 2, 7, 8, 16, 64
+    rng = np.random.default_rng(6 + C)
+    N, Hv = 2, H - 1
     x = rng.standard_normal((N, H, W, C)).astype(np.float32)
     w = (rng.standard_normal((3, C)) * 0.2).astype(np.float32)
     b = rng.standard_normal(3).astype(np.float32)
@@ -375,6 +380,18 @@ def test_head(dt):
     close(host(dw), dz.reshape(-1, 3).T @ xr.reshape(-1, C), "f32", "head dw")
     close(host(db), dz.reshape(-1, 3).sum(0), "f32", "head db")
     close(host(dx).reshape(dx_ref.shape) * 1e3, dx_ref * 1e3, dt, "head dx")
+    # the rank-3 gradient form: g3 = dz per pixel (zeros on the padding rows), same sums
+    g3 = torch.full((N * H * W * 3,), 7.0, device="cuda")
+    part3 = torch.empty(rows, 5 + 3 * C, device="cuda")
+    ops.head_fwd_bwd_g3(d, xv, Hv, cu(w), cu(b), cu(t), g3, part3)
+    la3, dw3, db3 = torch.empty(2, device="cuda"), torch.empty(3, C, device="cuda"), torch.empty(3, device="cuda")
+    ops.head_finalize(part3, rows, C, N * Hv * W * 3, la3, dw3, db3)
+    g3_ref = np.zeros((N, H, W, 3))
+    g3_ref[:, :Hv] = dz
+    torch.cuda.synchronize()
+    close(g3.cpu().numpy().reshape(g3_ref.shape) * 1e3, g3_ref * 1e3, "f32", "head g3")
+    assert np.array_equal(la3.cpu().numpy(), la.cpu().numpy())
+    assert np.array_equal(host(dw3), host(dw)) and np.array_equal(host(db3), host(db))
 
 
 def test_rmsprop():

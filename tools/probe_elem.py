@@ -39,6 +39,11 @@ def main():
     t = timeit(lambda: ops.head_fwd_bwd_g3(dt, x, Hv, wt, b, target, g3, part, aff=(sc, sh)))
     gb = (P * C * 2 + B * Hv * W * 12 + P * 12) / 1e9
     print(f"head_fwd_bwd_g3   {t:7.3f} ms  {gb / t:6.2f} TB/s (algorithmic {gb:.1f} GB)", flush=True)
+    y = torch.empty_like(x.buf)
+    t = timeit(lambda: y.copy_(x.buf))
+    gb = 2 * P * C * 2 / 1e9
+    print(f"torch copy (ref)  {t:7.3f} ms  {gb / t:6.2f} TB/s (algorithmic {gb:.1f} GB)", flush=True)
+    del y
     coef = torch.rand(3 * C, device="cuda")
     dz = torch.empty(P * C, dtype=T, device="cuda")
     prow = ops.query("cnnitmo_bn_bwd_rows", P, C)
