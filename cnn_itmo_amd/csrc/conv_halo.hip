@@ -57,15 +57,21 @@ constexpr int PPC = (PROWS + 15) / 16;                            // patch piece
 constexpr int NPI = (PPC + NWAVE - 1) / NWAVE;                    // patch pieces per wave
 constexpr int PFT = 5;  // taps over which the next item's DMA pieces are issued
 
-template <int BN> struct HCfg {
+// RES: the workgroup's weights for the whole K (at most RCH chunks) stay resident in
+// LDS, loaded once per launch; a ring stage then holds the halo patch only.  For the
+// small-K layers (cin <= 64: level 1 and 2) the per-item weight pieces were half of
+// every stage's DMA.
+constexpr int RCH = 2;
+template <int BN, bool RES> struct HCfg {
   static constexpr int FN = BN / 16, FP = FN / 2;        // fragments / 32-column pairs
   static constexpr int BPC = KT * BN / 16;               // weight pieces
   static constexpr int NBI = (BPC + NWAVE - 1) / NWAVE;  // weight pieces per wave
-  static constexpr int L = NPI + NBI;                    // DMA instructions per wave per item
+  static constexpr int L = RES ? NPI : NPI + NBI;        // DMA instructions per wave per item
   static constexpr int PATCH = PPC * 1024;
-  static constexpr int STAGE = PATCH + BPC * 1024;
+  static constexpr int STAGE = RES ? PATCH : PATCH + BPC * 1024;
   static constexpr int ST = 2;
-  static constexpr int SCR = ST * STAGE;    // 1 KiB sink for the padding pieces
+  static constexpr int WRES = ST * STAGE;                   // resident weights (RES)
+  static constexpr int SCR = WRES + (RES ? RCH * BPC * 1024 : 0);  // 1 KiB sink for the padding pieces
   static constexpr int PAR = SCR + 1024;    // [3][BN] fp32 epilogue parameters
   static constexpr int UTB = PAR + 3 * BN * 4;  // [BN][8] fp32 border table
   static constexpr int SMEM = UTB + BN * 8 * 4;
@@ -84,9 +90,9 @@ struct HaloArgs {
   long tiles;
 };
 
-template <int BN, int EPI>
+template <int BN, int EPI, bool RES>
 __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
-  using C = HCfg<BN>;
+  using C = HCfg<BN, RES>;
   constexpr int FN = C::FN, FP = C::FP, L = C::L, NBI = C::NBI, STAGE = C::STAGE, ST = C::ST;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
@@ -193,7 +199,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     if (k < NPI) {
       const int gp = wave * NPI + k;
       dma::lds16(pvo[k], dma::rsrc(pbase), gp < PPC ? iPs + gp * 1024 : smem + C::SCR);
-    } else {
+    } else if constexpr (!RES) {
       const int gp = wave * NBI + (k - NPI);
       dma::lds16(boff[k - NPI], dma::rsrc(bbase), gp < C::BPC ? iPs + C::PATCH + gp * 1024 : smem + C::SCR);
     }
@@ -233,9 +239,9 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const bool ok = e.y0 + wave * RPW + rr < p.ho && e.x0 + col < p.wo && c >= p.bnb_c0 && c < p.bnb_c1;
     return ok ? (unsigned)((((long)rr * p.wo + col) * p.bnb_r_ld + (c - p.bnb_c0)) * 2) : OOB;
   };
-  auto compute = [&](int buf, bool pf) {
+  auto compute = [&](int buf, bool pf, int ch) {
     const char* Ps = smem + buf * STAGE;
-    const char* Bs = Ps + C::PATCH;
+    const char* Bs = RES ? smem + C::WRES + ch * (C::BPC * 1024) : Ps + C::PATCH;
     uint4 af[2][FM], bfr[2][FN];
     auto load = [&](int tap, int sl) {
       const int r = tap / 3, s = tap - 3 * (tap / 3);
@@ -393,6 +399,19 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     zero_acc();
   };
 
+  if constexpr (RES) {  // the resident weights: every chunk's pieces, then a full drain
+    for (int ch = 0; ch < nch; ++ch) {
+      const uintptr_t wb = (uintptr_t)(Wt + (size_t)n0 * K + ch * 32);
+      char* dst = smem + C::WRES + ch * (C::BPC * 1024);
+#pragma unroll
+      for (int i = 0; i < NBI; ++i) {
+        const int gp = wave * NBI + i;
+        dma::lds16(boff[i], dma::rsrc(wb), gp < C::BPC ? dst + gp * 1024 : smem + C::SCR);
+      }
+    }
+    dma::wait_vm<0>();
+    __syncthreads();
+  }
   // ST-stage ring over items (see the file comment for the vmcnt accounting)
   Pos ep = ip;  // position of the item being computed
   int issued = 0;
@@ -420,7 +439,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     if (pf) issue_prep(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
     const bool act = ep.y0 + wave * RPW < p.ho;
     if (act) {
-      compute(buf, pf);  // issues those loads between its taps
+      compute(buf, pf, ep.ch);  // issues those loads between its taps
     } else if (pf) {     // the wave's rows are all below the frame: no MFMAs, DMA share only
 #pragma unroll
       for (int q = 0; q < L; ++q) issue_piece(q);
@@ -512,6 +531,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 
 struct HaloPlan {
   int bn, epi;
+  bool res;
 };
 
 int halo_ncu() {
@@ -545,12 +565,18 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
   } else {
     pl.epi = (a.flags || a.bias || a.border || a.stats) ? 1 : 0;
   }
+  static const int res = [] {
+    const char* e = getenv("CNNITMO_HALO_RES");
+    return e ? atoi(e) : 1;
+  }();
+  pl.res = res && a.cin <= 32 * RCH;
   return true;
 }
 
 template <int BN, int EPI>
-void launch_cfg(const HaloArgs& h, int grid, hipStream_t s) {
-  hipLaunchKernelGGL((halo_conv_kernel<BN, EPI>), dim3(grid), dim3(NT), 0, s, h);
+void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
+  if (res) hipLaunchKernelGGL((halo_conv_kernel<BN, EPI, true>), dim3(grid), dim3(NT), 0, s, h);
+  else hipLaunchKernelGGL((halo_conv_kernel<BN, EPI, false>), dim3(grid), dim3(NT), 0, s, h);
 }
 
 int halo_streams(const FwdArgs& a, const HaloPlan& pl) { return halo_ncu() / (a.N / pl.bn); }
@@ -578,14 +604,14 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
   const int grid = halo_ncu();
   if (pl.epi == 2) {
-    if (pl.bn == 64) launch_cfg<64, 2>(h, grid, s);
-    else launch_cfg<32, 2>(h, grid, s);
+    if (pl.bn == 64) launch_cfg<64, 2>(h, pl.res, grid, s);
+    else launch_cfg<32, 2>(h, pl.res, grid, s);
   } else if (pl.epi == 1) {
-    if (pl.bn == 64) launch_cfg<64, 1>(h, grid, s);
-    else launch_cfg<32, 1>(h, grid, s);
+    if (pl.bn == 64) launch_cfg<64, 1>(h, pl.res, grid, s);
+    else launch_cfg<32, 1>(h, pl.res, grid, s);
   } else {
-    if (pl.bn == 64) launch_cfg<64, 0>(h, grid, s);
-    else launch_cfg<32, 0>(h, grid, s);
+    if (pl.bn == 64) launch_cfg<64, 0>(h, pl.res, grid, s);
+    else launch_cfg<32, 0>(h, pl.res, grid, s);
   }
   return cnnitmo_check_launch(what);
 }
@@ -594,7 +620,7 @@ const char* halo_name(const FwdArgs& a) {
   HaloPlan pl;
   if (!halo_plan(a, pl)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "halo_conv_kernel<%d,%d>", pl.bn, pl.epi);
+  snprintf(buf, sizeof(buf), "halo_conv_kernel<%d,%d%s>", pl.bn, pl.epi, pl.res ? ",wres" : "");
   return buf;
 }
 
