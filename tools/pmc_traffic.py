@@ -37,9 +37,9 @@ def unmangle(n):
 
 def label(name):
     n = unmangle(name.replace(" ", "")).replace("(anonymousnamespace)::", "")
-    m = re.search(r"halo_conv_kernel<(\d+),(\d+)>", n)
+    m = re.search(r"halo_conv_kernel<(\d+),(\d+)(?:,(true|false))?>", n)
     if m:
-        return "halo_conv_kernel<%s,%s>" % m.groups()
+        return "halo_conv_kernel<%s,%s%s>" % (m.group(1), m.group(2), ",wres" if m.group(3) == "true" else "")
     m = re.search(r"halo_gemm_kernel<(\d+),(\d+),(\d+),(\d+),\d+(?:,(\d+))?>", n)
     if m:
         return "halo_gemm_kernel<%s,%s,%s,%s%s>" % (m.groups()[:4] + (",bnb" if m.group(5) not in (None, "0") else "",))
