@@ -50,7 +50,13 @@ namespace {
 
 using dma::OOB;
 
-constexpr int TH = 16, TW = 32, NWAVE = 8, NT = NWAVE * 64;
+// 8 waves (2 per SIMD, 64 x BN wave tiles).  HALO_NWAVE=4 (1 per SIMD, 128 x BN wave
+// tiles, accumulators in AGPRs, 25 % fewer LDS fragment reads per MFMA) compiles and
+// measured 8-10 % slower on every layer: one wave per SIMD does not hide the latencies.
+#ifndef HALO_NWAVE
+#define HALO_NWAVE 8
+#endif
+constexpr int TH = 16, TW = 32, NWAVE = HALO_NWAVE, NT = NWAVE * 64;
 constexpr int RPW = TH / NWAVE, FMR = TW / 16, FM = RPW * FMR;  // tile rows / fragments per wave
 constexpr int KT = 9, PW = TW + 2, PROWS = (TH + 2) * PW;         // halo patch: 18 x 34 rows of 64 B
 constexpr int PPC = (PROWS + 15) / 16;                            // patch pieces (1 KiB = 16 rows)
