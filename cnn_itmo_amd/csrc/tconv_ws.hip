@@ -281,8 +281,10 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl) {
   if (nblk > 32 || 32 % nblk) return false;
   // where it measured faster than the halo / implicit-GEMM paths (tools/ab_env.sh,
   // b32 1080p): every forward at BN 128 (up6 1.50 -> 1.08, up7 2.62 -> 1.98, up8
-  // 3.16 -> 2.98 ms) and the gradient at BN 128 (up8: 2.48 -> 1.87 ms); at BN 64
-  // (up7 gradient, K = 1024) the A fragments re-read from L2 per 4 MFMAs bound it.
+  // 3.16 -> 2.98 ms) and the gradient at BN 128 (up8: 2.48 -> 1.87 ms).  The up7
+  // gradient (K = 1024) needs BN 64: with 32-pixel tiles the A re-reads bound it, and
+  // with 64-pixel tiles (the same A loads per MFMA as BN 128) it measured 2.15 ms
+  // against igemm_fwd2's 1.90.
   if (bn != 128) return false;
   pl.bn = bn;
   pl.nblk = nblk;
