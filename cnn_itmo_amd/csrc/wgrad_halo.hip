@@ -314,6 +314,10 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
   return true;
 }
 
+// Timing-only builds of the 64 x 96 block (dec6-dec9; garbage results, tools/ build):
+// no s_barrier -11 %, no vmcnt wait -11 %, no row DMA -15 %, none of the three -24 %
+// (1.15 -> 1.5 PF/s: the MFMA + fragment-read loop alone).  Prefetching 4 rows ahead
+// instead of 2 changed nothing: the row DMA's issue/LDS-write cost, not its latency.
 template <int BM, int BN, int TW>
 void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
   // 12 waves (3 per SIMD) for the big blocks, 6 for the small ones
