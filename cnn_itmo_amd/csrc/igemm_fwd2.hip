@@ -324,6 +324,14 @@ void launch_st(const FwdArgs& a, hipStream_t s, dim3 grid) {
 }  // namespace
 
 int fwd2_stat_rows(long m) { return (int)((m + 255) / 256); }
+
+bool fwd2_tconv_bm128(const FwdArgs& a) {
+  static const int en = [] {
+    const char* e = getenv("CNNITMO_FWD2_BM128");
+    return e ? atoi(e) : 1;
+  }();
+  return en && a.N % 128 == 0 && a.ntaps == 4 && a.scale == 2 && !a.stats;
+}
 bool fwd2_handles(int N) { return N != 32; }
 
 template <typename T>
@@ -336,6 +344,19 @@ int launch_fwd2(FwdArgs a, hipStream_t s, const char* what) {
   CNN_REQUIRE(!a.scatter || a.cout % VE == 0, "%s: scatter needs cout %% %d == 0", what, VE);
   CNN_REQUIRE(a.M > 0 && a.ntaps >= 1 && a.ntaps <= 9, "%s: bad sizes", what);
   const Cfg2 c = pick2(a.N);
+  // the bf16 Conv2DTranspose input gradient (4-tap stride-2 gather, no epilogue sums):
+  // 128 x 128 tiles with a 2-deep ring (64 KB) run two workgroups per CU, so one
+  // workgroup's prologue and LDS-staged epilogue overlap the other's MFMAs
+  if constexpr (sizeof(T) == 2) {
+    if (fwd2_tconv_bm128(a)) {
+      a.mblocks = (int)((a.M + 127) / 128);
+      a.nblocks = a.N / 128;
+      CNN_REQUIRE((long)a.mblocks * a.nblocks < (1L << 31), "%s: grid too large", what);
+      hipLaunchKernelGGL((igemm_fwd2_kernel<T, 128, 128, 2, 4, 2>), dim3((unsigned)(a.mblocks * a.nblocks)),
+                         dim3(512), 0, s, a);
+      return cnnitmo_check_launch(what);
+    }
+  }
   a.mblocks = (int)((a.M + 255) / 256);
   a.nblocks = a.N / c.bn;
   const long total = (long)a.mblocks * a.nblocks;
