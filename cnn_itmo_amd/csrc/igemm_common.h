@@ -86,7 +86,7 @@ template <typename T>
 int launch_fwd2(FwdArgs a, hipStream_t s, const char* what);
 int fwd2_stat_rows(long m);
 bool fwd2_handles(int N);  // v2 is the faster kernel for this column count
-bool fwd2_tconv_bm128(const FwdArgs& a);  // bf16 tconv input gradient: 128 x 128 tiles
+int fwd2_bm(const FwdArgs& a, bool bf16);  // row tile of the v2 launch (128 or 256)
 
 // halo-tiled 3x3 conv (bf16, 4x64 output tiles), conv_halo.hip
 bool halo_handles(const FwdArgs& a);

@@ -391,7 +391,7 @@ extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int 
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
   if (!use_v1() && fwd2_handles(a.N)) {
     const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
-    snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,256x%d>", t, bn);
+    snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,%dx%d>", t, fwd2_bm(a, dtype == CNNITMO_BF16), bn);
   } else {
     const Cfg c = pick_cfg(a.N);
     snprintf(buf, sizeof(buf), "igemm_fwd_kernel<%s,%dx%d>", t, c.bm, c.bn);
@@ -418,7 +418,7 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
   if (!use_v1() && fwd2_handles(a.N)) {
     const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
-    const int bm = dtype == CNNITMO_BF16 && fwd2_tconv_bm128(a) ? 128 : 256;
+    const int bm = fwd2_bm(a, dtype == CNNITMO_BF16);
     snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,%dx%d>", t, bm, bn);
   } else {
     const Cfg c = pick_cfg(a.N);

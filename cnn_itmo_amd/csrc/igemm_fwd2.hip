@@ -325,12 +325,19 @@ void launch_st(const FwdArgs& a, hipStream_t s, dim3 grid) {
 
 int fwd2_stat_rows(long m) { return (int)((m + 255) / 256); }
 
-bool fwd2_tconv_bm128(const FwdArgs& a) {
+// Row tile of the v2 launch: 128 x 128 tiles with a 2-deep ring (64-68 KB, two
+// workgroups per CU: one workgroup's prologue and LDS-staged epilogue overlap the
+// other's MFMAs) for the bf16 Conv2DTranspose input gradient (up6/up7 0.87/1.93 ->
+// 0.83/1.81 ms) and for every fp32 launch with N % 128 == 0 (inference dec6-dec8
+// 15.4-15.8 -> 15.0-15.3 ms); launches with BN partial sums keep 256-row tiles (the
+// sums rows are per 256 rows).  CNNITMO_FWD2_BM128=0: 256 everywhere.
+int fwd2_bm(const FwdArgs& a, bool bf16) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_FWD2_BM128");
     return e ? atoi(e) : 1;
   }();
-  return en && a.N % 128 == 0 && a.ntaps == 4 && a.scale == 2 && !a.stats;
+  if (!en || a.N % 128 || a.stats) return 256;
+  return (!bf16 || (a.ntaps == 4 && a.scale == 2)) ? 128 : 256;
 }
 bool fwd2_handles(int N) { return N != 32; }
 
@@ -344,11 +351,8 @@ int launch_fwd2(FwdArgs a, hipStream_t s, const char* what) {
   CNN_REQUIRE(!a.scatter || a.cout % VE == 0, "%s: scatter needs cout %% %d == 0", what, VE);
   CNN_REQUIRE(a.M > 0 && a.ntaps >= 1 && a.ntaps <= 9, "%s: bad sizes", what);
   const Cfg2 c = pick2(a.N);
-  // the bf16 Conv2DTranspose input gradient (4-tap stride-2 gather, no epilogue sums):
-  // 128 x 128 tiles with a 2-deep ring (64 KB) run two workgroups per CU, so one
-  // workgroup's prologue and LDS-staged epilogue overlap the other's MFMAs
-  if constexpr (sizeof(T) == 2) {
-    if (fwd2_tconv_bm128(a)) {
+  if (fwd2_bm(a, sizeof(T) == 2) == 128) {
+    {
       a.mblocks = (int)((a.M + 127) / 128);
       a.nblocks = a.N / 128;
       CNN_REQUIRE((long)a.mblocks * a.nblocks < (1L << 31), "%s: grid too large", what);
