@@ -46,7 +46,7 @@ def label(name):
     m = re.search(r"tconv_stream_kernel<(\d+),(\d+),\d+,(true|false)>", n)
     if m:
         return "tconv_stream_kernel<%s,%s%s>" % (m.group(1), m.group(2), ",bnb" if m.group(3) == "true" else "")
-    m = re.search(r"tconv_ws_kernel<(\d+),(\d+)>", n)
+    m = re.search(r"tconv_ws_kernel<(\d+),(\d+)(?:,\d+)*>", n)
     if m:
         return "tconv_ws_kernel<%s,%s>" % m.groups()
     m = re.search(r"wgrad_halo_kernel<(\d+),(\d+),(\d+),", n)
