@@ -57,23 +57,24 @@ struct WHArgs {
 
 // Waves: three groups (one per kernel row r = 0, 1, 2), each WM x WN over the
 // (BM, BN) block, so every wave keeps 3 taps x its tile in accumulators.
-template <int BM, int BN, int TW, int WM, int WN, int D>
+// D: groups (dz row + x row) issued ahead; R: rows per barrier step
+template <int BM, int BN, int TW, int WM, int WN, int D, int R>
 struct WHCfg {
   static constexpr int NWG = WM * WN, NW = 3 * NWG, NT = NW * 64;
   static constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16, KS = TW / 32;
   static constexpr int XROWS = TW + 2;
   static constexpr int XB = (XROWS * BN * 2 + 1023) / 1024;  // KB (= DMA instructions) per x row
   static constexpr int DB = TW * BM * 2 / 1024;              // per dz row
-  static constexpr int XS = D + 3, DS = D + 1;               // ring slots
+  static constexpr int XS = D + R + 2, DS = D + R;           // ring slots
   static constexpr int SMEM = ((XS + 1) * XB + DS * DB) * 1024;  // + one all-zero x row
   static constexpr int LX = (XB + NW - 1) / NW, LD = (DB + NW - 1) / NW;  // max DMA per wave per row
   static_assert(TW * BM * 2 % 1024 == 0, "dz rows must be whole KB");
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
-template <int BM, int BN, int TW, int WM, int WN, int D>
+template <int BM, int BN, int TW, int WM, int WN, int D, int R>
 __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHArgs p) {
-  using C = WHCfg<BM, BN, TW, WM, WN, D>;
+  using C = WHCfg<BM, BN, TW, WM, WN, D, R>;
   constexpr int NW = C::NW, TM = C::TM, TN = C::TN, FM = C::FM, FN = C::FN, KS = C::KS;
   constexpr int XB = C::XB, DB = C::DB, XS = C::XS, DS = C::DS, LX = C::LX, LD = C::LD;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
@@ -162,51 +163,41 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
   // (ordered before the first use by the loop's barrier)
 
   // ---- pipeline: group k = {dz row g0+k, x row g0+k+1}; x rows g0-1, g0 first --
+  // D groups are issued ahead; each step (one vmcnt wait + one barrier) multiplies R
+  // rows and then issues the R groups that refill the slots of the previous step
   int issued = 0;
-  int mq[D + 1];
+  int gq[D + R];  // gq[j]: value of `issued` once group k + j is issued
   int xslot_next = 0;  // slot for the next x row to issue (rows issued in order from g0-1)
   int dslot_next = 0;
+  auto issue_group = [&](int j) {
+    issue_d(g0 + j, dslot_next);
+    dslot_next = dslot_next + 1 == DS ? 0 : dslot_next + 1;
+    issue_x(g0 + j + 1, xslot_next);
+    xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+    issued += nd + nx;
+  };
   issue_x(g0 - 1, xslot_next);
   xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
   issue_x(g0, xslot_next);
   xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
   issued += 2 * nx;
 #pragma unroll
-  for (int k = 0; k <= D; ++k) mq[k] = issued;
-#pragma unroll
-  for (int k = 0; k < D; ++k) {
-    if (k < nrows) {
-      issue_d(g0 + k, dslot_next);
-      dslot_next = dslot_next + 1 == DS ? 0 : dslot_next + 1;
-      issue_x(g0 + k + 1, xslot_next);
-      xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
-      issued += nd + nx;
-    }
-    mq[k] = issued;
+  for (int j = 0; j < D + R; ++j) {
+    if (j < D && j < nrows) issue_group(j);
+    gq[j] = issued;
   }
   int xs0 = 0;  // slot of x row g0+k-1
   int ds0 = 0;  // slot of dz row g0+k
   int y = (int)(g0 % p.H);
-  for (int k = 0; k < nrows; ++k) {
-    dma::wait_vm_dyn(issued - mq[0]);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (k + D < nrows) {
-      issue_d(g0 + k + D, dslot_next);
-      dslot_next = dslot_next + 1 == DS ? 0 : dslot_next + 1;
-      issue_x(g0 + k + D + 1, xslot_next);
-      xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
-      issued += nd + nx;
-      mq[D] = issued;
-    }
-    // ---- compute row y: taps r = 0,1,2 read x rows y-1, y, y+1 (zero at the image edge)
-    const char* Ds = dbase + ds0 * DB * 1024;
-    const int xs1 = xs0 + 1 == XS ? 0 : xs0 + 1, xs2 = xs1 + 1 == XS ? 0 : xs1 + 1;
+  auto nxt = [](int sl, int n) { return sl + 1 == n ? 0 : sl + 1; };
+  // one row: taps r = 0,1,2 read x rows y-1, y, y+1 (zero at the image edge)
+  auto row = [&](int dsl, int xa, int yy) {
+    const char* Ds = dbase + dsl * DB * 1024;
+    const int xb = nxt(xa, XS), xc = nxt(xb, XS);
     // rows outside the image read the zero row (a uniform pointer select, no branch:
     // a skipped tap would make the compiler copy the accumulators around it)
-    const int xsr = wr == 0 ? xs0 : (wr == 1 ? xs1 : xs2);
-    const char* Xs = (wr == 0 && y == 0) || (wr == 2 && y == p.H - 1) ? zrow : xbase + xsr * XB * 1024;
+    const int xsr = wr == 0 ? xa : (wr == 1 ? xb : xc);
+    const char* Xs = (wr == 0 && yy == 0) || (wr == 2 && yy == p.H - 1) ? zrow : xbase + xsr * XB * 1024;
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       const int r0 = kk * 32 + 8 * g + qq;
@@ -218,30 +209,46 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + bfo<BM>(r0 + 4, col)));
         af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
-      {
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-          bf16x8 bfr[FN];
+      for (int s = 0; s < 3; ++s) {
+        bf16x8 bfr[FN];
 #pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            const int col = wn * TN + j * 16 + 4 * pp;
-            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s, col)));
-            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s + 4, col)));
-            bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          }
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-              acc[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[s][i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) {
+          const int col = wn * TN + j * 16 + 4 * pp;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s, col)));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s + 4, col)));
+          bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[s][i][j], 0, 0, 0);
+      }
+    }
+  };
+  for (int k = 0; k < nrows; k += R) {
+    const int last = nrows - k < R ? nrows - k - 1 : R - 1;  // rows k .. k+last this step
+    dma::wait_vm_dyn(issued - gq[last]);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (k + D + r < nrows) issue_group(k + D + r);
+      gq[D + r] = issued;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (r <= last) {
+        row(ds0, xs0, y);
+        xs0 = nxt(xs0, XS);
+        ds0 = nxt(ds0, DS);
+        y = y + 1 == p.H ? 0 : y + 1;
       }
     }
 #pragma unroll
-    for (int q = 0; q < D; ++q) mq[q] = mq[q + 1];
-    xs0 = xs1;
-    ds0 = ds0 + 1 == DS ? 0 : ds0 + 1;
-    y = y + 1 == p.H ? 0 : y + 1;
+    for (int q = 0; q < D; ++q) gq[q] = gq[q + R];
   }
 
   // ---- this workgroup's slab: [cout][9][cin] (its BM x BN block) ----------------
@@ -259,6 +266,17 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
           O[(size_t)co * 9 * p.cin + t * p.cin + n0 + wn * TN + j * 16 + li] = acc[s][i][j][rr];
       }
 }
+
+// Rows per barrier step.  Timing-only builds of the 64 x 96 block (dec6-dec9; garbage
+// results): no s_barrier -11 %, no vmcnt wait -11 %, no row DMA -15 %, none of the
+// three -24 % (1.15 -> 1.5 PF/s: the MFMA + fragment-read loop alone); prefetching 4
+// rows ahead instead of 2 changed nothing.  So the 64 x 96 block (one workgroup per CU
+// at any ring size) multiplies two rows per wait + barrier, 3 groups ahead (144 KB);
+// the smaller blocks keep one row per step (two workgroups per CU).
+#ifndef WH_ROWS96
+#define WH_ROWS96 2
+#endif
+constexpr int wh_rows(int bm, int bn) { return bm == 64 && bn == 96 ? WH_ROWS96 : 1; }
 
 struct WHPlan {
   int bm, bn, tw, strips, cbm, cbn, rsplits, smem;
@@ -297,7 +315,8 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
     if (ncu <= 0) ncu = 256;
   }
   const int xb = ((pl.tw + 2) * pl.bn * 2 + 1023) / 1024, db = pl.tw * pl.bm * 2 / 1024;
-  const int smem = (6 * xb + 3 * db) * 1024;  // D = 2
+  const int R = wh_rows(pl.bm, pl.bn), D = R == 2 ? 3 : 2;
+  const int smem = ((D + R + 3) * xb + (D + R) * db) * 1024;  // WHCfg::SMEM
   const int occ = std::max(1, (160 * 1024) / smem);
   const long slots = (long)ncu * occ;
   long best = 1;
@@ -314,15 +333,12 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
   return true;
 }
 
-// Timing-only builds of the 64 x 96 block (dec6-dec9; garbage results, tools/ build):
-// no s_barrier -11 %, no vmcnt wait -11 %, no row DMA -15 %, none of the three -24 %
-// (1.15 -> 1.5 PF/s: the MFMA + fragment-read loop alone).  Prefetching 4 rows ahead
-// instead of 2 changed nothing: the row DMA's issue/LDS-write cost, not its latency.
 template <int BM, int BN, int TW>
 void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
   // 12 waves (3 per SIMD) for the big blocks, 6 for the small ones
   constexpr int WM = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1), WN = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2);
-  hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, 2>), dim3(grid), dim3(3 * WM * WN * 64), 0, s, a);
+  constexpr int R = wh_rows(BM, BN), D = R == 2 ? 3 : 2;
+  hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R>), dim3(grid), dim3(3 * WM * WN * 64), 0, s, a);
 }
 
 }  // namespace
