@@ -61,13 +61,9 @@ constexpr int RPW = TH / NWAVE, FMR = TW / 16, FM = RPW * FMR;  // tile rows / f
 constexpr int KT = 9, PW = TW + 2, PROWS = (TH + 2) * PW;         // halo patch: 18 x 34 rows of 64 B
 constexpr int PPC = (PROWS + 15) / 16;                            // patch pieces (1 KiB = 16 rows)
 constexpr int NPI = (PPC + NWAVE - 1) / NWAVE;                    // patch pieces per wave
-#ifndef HALO_PFT
-#define HALO_PFT 5
-#endif
-#ifndef HALO_PRIO
-#define HALO_PRIO 0
-#endif
-constexpr int PFT = HALO_PFT;  // taps over which the next item's DMA pieces are issued
+// taps over which the next item's DMA pieces are issued (3 and 8 measured no better,
+// profiles/r02l_ab_halo_knobs.txt)
+constexpr int PFT = 5;
 
 // RES: the workgroup's weights for the whole K (at most RCH chunks) stay resident in
 // LDS, loaded once per launch; a ring stage then holds the halo patch only.  For the
@@ -271,12 +267,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       const int cur = tap & 1;
       if (tap + 1 < KT) load(tap + 1, cur ^ 1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (HALO_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], bfr[cur][j], af[cur][i]);  // C^T: lanes = pixels
-      if constexpr (HALO_PRIO) __builtin_amdgcn_s_setprio(0);
       if (pf) {
 #pragma unroll
         for (int k = 0; k < L; ++k)
