@@ -10,7 +10,7 @@ Here the same conventions run batched on the GPU:
 
     python -m cnn_itmo_amd.predict --model saved7-model-218-0.73.hdf5 \\
         [--input images_to_predict/input] [--output images_to_predict/output] \\
-        [--batch 8] [--dtype float32|bfloat16]
+        [--batch 8] [--dtype float32|bfloat16] [--tile TH,TW]
 
 Differences, all deliberate: images are processed in sorted order, in batches
 of equal-sized frames; the output file name is the input's base name (the
@@ -77,9 +77,19 @@ def _pad_cols(x, W):
     return out
 
 
-def predict_frames(model, frames_u8, batch=8, cache=None):
-    """uint8 frames (equal sizes) -> uint8 predictions, reference conventions."""
+def predict_frames(model, frames_u8, batch=8, cache=None, tile=None):
+    """uint8 frames (equal sizes) -> uint8 predictions, reference conventions.
+    ``tile`` (th, tw): spatially tiled inference with 96-px halos (tiled.py; same
+    result, activation memory bounded by the window instead of the frame)."""
     h, w = frames_u8[0].shape[:2]
+    if tile is not None:
+        from .tiled import predict_tiled
+        outs = []
+        for i in range(0, len(frames_u8), batch):
+            x = np.stack([to_input(f) for f in frames_u8[i:i + batch]])
+            y = predict_tiled(model, x, tile, batch_size=batch, cache=cache)
+            outs.extend(to_png(y[j]) for j in range(y.shape[0]))
+        return outs
     m = model_for_size(model, h, w, cache)
     W = m.inputs[0].shape[1]
     outs = []
@@ -90,7 +100,7 @@ def predict_frames(model, frames_u8, batch=8, cache=None):
     return outs
 
 
-def predict_dir(model, in_dir, out_dir, batch=8, pattern="*.png", log=print):
+def predict_dir(model, in_dir, out_dir, batch=8, pattern="*.png", log=print, tile=None):
     from PIL import Image
     files = sorted(glob.glob(os.path.join(in_dir, pattern)))
     if not files:
@@ -104,7 +114,7 @@ def predict_dir(model, in_dir, out_dir, batch=8, pattern="*.png", log=print):
     written = []
     for shape, fs in groups.items():
         log(f"Grabbing {len(fs)} input files of {shape[1]}x{shape[0]}")
-        preds = predict_frames(model, [frames[f] for f in fs], batch, cache)
+        preds = predict_frames(model, [frames[f] for f in fs], batch, cache, tile)
         for f, p in zip(fs, preds):
             dst = os.path.join(out_dir, os.path.basename(f))
             Image.fromarray(p).save(dst)
@@ -119,13 +129,15 @@ def main(argv=None):
     ap.add_argument("--output", default="images_to_predict/output")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--dtype", default="float32", choices=["float32", "bfloat16"])
+    ap.add_argument("--tile", default=None, help="TH,TW: spatially tiled inference (multiples of 16; 96-px halos)")
     a = ap.parse_args(argv)
+    tile = tuple(int(v) for v in a.tile.split(",")) if a.tile else None
     from .model import load_model
     m = load_model(a.model)
     if m.optimizer is None:
         m.compile(optimizer="rmsprop", loss="mse", metrics=["accuracy"])
     m.set_dtype(a.dtype)
-    out = predict_dir(m, a.input, a.output, a.batch)
+    out = predict_dir(m, a.input, a.output, a.batch, tile=tile)
     print(f"wrote {len(out)} predictions to {a.output}")
     return 0
 
