@@ -55,6 +55,7 @@ class Value:
         self.members = []  # for concat values: placed member Values
         self.buf = None
         self.gbuf = None
+        self.gsep = False  # gradient in a dense buffer of its own, not the concat owner's slice
         self.ginit = False
         self.needs_grad = True
         self.folded = False  # holds r; the true value is r*cs + ch (per channel)
@@ -77,7 +78,7 @@ class Value:
         return ops.View(self.buf, n, self.h, self.w, self.c, self.c, 0)
 
     def gview(self, n):
-        if self.place:
+        if self.place and not self.gsep:
             cv, off = self.place
             return ops.View(cv.gbuf, n, self.h, self.w, self.c, cv.c, off)
         return ops.View(self.gbuf, n, self.h, self.w, self.c, self.c, 0)
@@ -88,7 +89,7 @@ class Value:
             o.buf = torch.empty(n * o.h * o.w * o.c, dtype=dtype, device=device)
 
     def ensure_grad(self, n, dtype, device, zero=False):
-        o = self.owner()
+        o = self if self.gsep else self.owner()
         if o.gbuf is None:
             o.gbuf = (torch.zeros if zero else torch.empty)(n * o.h * o.w * o.c, dtype=dtype, device=device)
             if zero:
@@ -379,6 +380,18 @@ class BlockStage(Stage):
                     return m, ci0, rows
         return None
 
+    def _skip_member(self, ci0):
+        """The concat member holding input channels [0, ci0) when it is exactly one value
+        without a gradient yet (dec9's `conv1`, 64 B of every 192-B row): the split dgrad
+        then writes its gradient to a dense buffer of its own (CNNITMO_DENSE_SKIP=0: into
+        the concat's gradient slice).  Nothing reads that gradient through the concat."""
+        if os.environ.get("CNNITMO_DENSE_SKIP", "1") == "0":
+            return None
+        ms = [v for v in self.vin.members if v.place and v.place[1] < ci0]
+        if len(ms) == 1 and ms[0].place[1] == 0 and ms[0].c == ci0 and not ms[0].ginit:
+            return ms[0]
+        return None
+
     def _split_fused(self, ci0, c):
         """dec9's input gradient (concat [skip 32 | up 64], model.py:261): two launches
         -- the skip columns as a plain 32-column dgrad and the up columns as a 64-column
@@ -443,19 +456,28 @@ class BlockStage(Stage):
             prod = m.producer
             coef = prod.bn_coef(n)
             whole = ci0 == 0 and m.c == self.cin
+            split = self.kind == "c3" and self._split_fused(ci0, m.c)
+            skip = self._skip_member(ci0) if split else None
             dx = None
             if not whole:
                 if self.vin.ginit:
                     raise NotImplementedError(f"{self.name}: input gradient would need accumulation")
-                self.vin.ensure_grad(n, e.tdtype, e.device)
-                dx = self.vin.gview(n)
+                if skip is None:
+                    self.vin.ensure_grad(n, e.tdtype, e.device)
+                    dx = self.vin.gview(n)
             ppar = prod.fold_active and prod.kind == "t2"
             pin = n * self.vin.h * self.vin.w
             dzp = torch.empty(pin * m.c, dtype=e.tdtype, device=e.device)
             pp = torch.empty(frows * (4 if ppar else 1) * m.c, device=e.device, dtype=torch.float32)
-            if self.kind == "c3" and self._split_fused(ci0, m.c):
+            if split:
                 h, w = self.vout.h, self.vout.w
-                ops.conv3x3_dgrad(e.dt, dz, n, h, w, cout, self.w_bwd, ci0, ops.View(dx.buf, n, h, w, ci0, dx.ld, dx.off))
+                if skip is not None:  # dense skip gradient: full-line traffic for the pool / BN backward
+                    skip.gsep = True
+                    skip.ensure_grad(n, e.tdtype, e.device)
+                    dxs = skip.gview(n)
+                else:
+                    dxs = ops.View(dx.buf, n, h, w, ci0, dx.ld, dx.off)
+                ops.conv3x3_dgrad(e.dt, dz, n, h, w, cout, self.w_bwd, ci0, dxs)
                 wsub = self.w_bwd[ci0 * 9 * cout:]  # flipped weights [cin][3][3][cout]: rows ci0..
                 ops.conv3x3_dgrad_bn(e.dt, dz, n, h, w, cout, wsub, m.c, None, 0, m.c, coef, prod.r, dzp, pp, ppar)
             elif self.kind == "c3":
