@@ -73,7 +73,8 @@ class KernelTimer:
     def __init__(self, ops, torch):
         self.ops, self.torch = ops, torch
         self.on = False
-        self.rec = []  # (name, flops, ev0, ev1)
+        self.rec = []  # (name, flops, ev0, ev1, tag, algorithmic bytes)
+        self._nb = 0  # algorithmic HBM bytes of the next bracketed launch (conv3x3 fwd only)
         self._pool, self._next = [], 0
         self._wrap()
 
@@ -87,6 +88,7 @@ class KernelTimer:
         return f"igemm_fwd2_kernel<{t},256x{bn}>"
 
     def _bracket(self, name, flops, tag, fn, *a, **k):
+        nb, self._nb = self._nb, 0
         if not self.on:
             return fn(*a, **k)
         i = self._next
@@ -97,7 +99,7 @@ class KernelTimer:
         e0.record()
         r = fn(*a, **k)
         e1.record()
-        self.rec.append((name, flops, e0, e1, tag))
+        self.rec.append((name, flops, e0, e1, tag, nb))
         return r
 
     def reset(self):
@@ -116,6 +118,8 @@ class KernelTimer:
 
         def conv3x3_fwd(dt, x, wt, bias, out, *a, **k):
             fl = 2.0 * x.p * out.c * 9 * x.c
+            # single-pass bytes: the input view once, the output once, the weights once (also tconv_fwd)
+            self._nb = (2 if dt == 1 else 4) * (x.p * x.c + x.p * out.c + 9 * x.c * out.c)
             return self._bracket(kname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, f"fwd {x.h}x{x.w} {x.c}->{out.c}", o["conv3x3_fwd"], dt, x, wt, bias,
                                  out, *a, **k)
 
@@ -140,6 +144,7 @@ class KernelTimer:
 
         def tconv_fwd(dt, x, k_, bias, out, *a, **k):
             fl = 2.0 * x.p * 4 * out.c * x.c
+            self._nb = (2 if dt == 1 else 4) * (x.p * x.c + 4 * x.p * out.c + 4 * x.c * out.c)
             return self._bracket(tname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, f"t.fwd {x.h}x{x.w} {x.c}->{out.c}", o["tconv_fwd"], dt, x, k_, bias, out,
                                  *a, **k)
 
@@ -183,7 +188,7 @@ class KernelTimer:
     def detail(self):
         """(name, launch tag) -> [launches, flops, ms]: per-layer view of the same events."""
         agg = {}
-        for name, fl, e0, e1, tag in self.rec:
+        for name, fl, e0, e1, tag, _ in self.rec:
             a = agg.setdefault((name, tag), [0, 0.0, 0.0])
             a[0] += 1
             a[1] += fl
@@ -192,12 +197,14 @@ class KernelTimer:
 
     def summary(self):
         agg = {}
-        for name, fl, e0, e1, _ in self.rec:
+        for name, fl, e0, e1, _, nb in self.rec:
             ms = e0.elapsed_time(e1)
-            a = agg.setdefault(name, [0, 0.0, 0.0])
+            a = agg.setdefault(name, [0, 0.0, 0.0, 0.0, 0])
             a[0] += 1
             a[1] += fl
             a[2] += ms
+            a[3] += nb
+            a[4] += 1 if nb else 0
         return agg
 
 
@@ -273,7 +280,9 @@ def _spawn_ranks(args):
 # ---------------------------------------------------------------- legs
 def _roofline(agg, steps, elapsed, peak):
     dom = max(agg.items(), key=lambda kv: kv[1][2])
-    name, (cnt, fl, ms) = dom
+    name, (cnt, fl, ms, nbytes, nbcnt) = dom
+    if nbcnt != cnt:  # bytes are accounted for the conv3x3 / tconv forwards only
+        nbytes = 0
     achieved = fl / (ms * 1e-3) / 1e12
     step_flops = sum(v[1] for v in agg.values()) / steps
     traffic = None
@@ -288,12 +297,16 @@ def _roofline(agg, steps, elapsed, peak):
             "frac": round(achieved / peak, 4), "traffic": traffic,
             "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
             "algorithmic_flop_per_launch": fl / cnt,
+            # single-pass HBM bytes (input, output, weights once) per launch, and the
+            # measured traffic over it (re-read factor)
+            "algorithmic_bytes_per_launch": nbytes / cnt if nbytes else None,
+            "traffic_over_algorithmic": round(traffic / (nbytes / cnt), 3) if traffic and nbytes else None,
             "step_conv_tflops": round(step_flops / (elapsed / steps) / 1e12, 2),
             "step_mfma_frac": round(step_flops / (elapsed / steps) / 1e12 / peak, 4)}, step_flops
 
 
 def _print_agg(agg, tag):
-    for k, (c, f, m) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
+    for k, (c, f, m, _, _) in sorted(agg.items(), key=lambda kv: -kv[1][2]):
         print(f"[bench:{tag}] {k:55s} launches={c:5d} time={m:9.1f} ms  {f / (m * 1e-3) / 1e12:7.1f} TFLOP/s",
               file=sys.stderr)
 
