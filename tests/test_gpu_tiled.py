@@ -49,9 +49,9 @@ def test_tiled_equals_full_frame(dtype, shape, tile):
     tiled = predict_tiled(m, x, tile, batch_size=4)
     assert tiled.shape == (2, h, w, 3)
     d = np.abs(tiled - full)
-    # the same kernels compute every pixel in the same order: identical up to fp32
-    # accumulation-order noise (the bound is far below one bf16 / uint8 step)
-    assert float(d.max()) <= 1e-6, (dtype, float(d.max()), float((d > 0).mean()))
+    # the same kernels compute every pixel's dot products in the same order wherever the
+    # pixel sits in its launch: the tiled result is bit-identical
+    assert float(d.max()) == 0.0, (dtype, float(d.max()), float((d > 0).mean()))
 
 
 def test_predict_cli_tiled(tmp_path):
@@ -72,4 +72,4 @@ def test_predict_cli_tiled(tmp_path):
         a = np.asarray(Image.open(str(tmp_path / "a" / f"{i}.png"))).astype(int)
         b = np.asarray(Image.open(str(tmp_path / "b" / f"{i}.png"))).astype(int)
         assert a.shape == b.shape == (270, 300, 3)
-        assert np.abs(a - b).max() <= 1 and (a != b).mean() < 1e-4
+        assert np.array_equal(a, b)
