@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--k4-batch", type=int, default=8,
                     help="4K bf16 training leg (configs[4]: 3840x2160, global 64 on 8 GPUs) frames per GPU; 0 = skip")
     ap.add_argument("--k4-steps", type=int, default=4)
+    ap.add_argument("--ns-batch", type=int, default=32,
+                    help="north-star leg: fp32 1080p inference (conv2d forward) at this batch per GPU; 0 = skip")
     return ap.parse_args()
 
 
@@ -256,7 +258,40 @@ def cpu_baseline(args, P_init, H, W, train=True):
             "cores": blas, "kind": "port",
             "sample": f"oracle/unet_ref.py numpy fp32 {what} on 1 frame {w}x{h} "
                       f"({frac:.4f} of a 1920x{H} frame, scaled by pixel count); {dt:.2f} s",
-            "seconds": dt, "affinity_cores": cores, "blas_threads": blas, "cpu_model": model}
+            "seconds": dt, "affinity_cores": cores, "blas_threads": blas, "cpu_model": model,
+            "threads_note": THREADS_NOTE}
+
+
+# `cores` is the BLAS thread count actually used.  The GPU box allots 16 host CPUs per
+# GPU (the harness exports OMP_NUM_THREADS=16 and asks for pools of at most 16);
+# sched_getaffinity there lists every core of the host (256), which are not ours.
+THREADS_NOTE = ("BLAS threads = the box's CPU share per GPU (OMP_NUM_THREADS, 16 on the MI355X box); "
+                "affinity_cores counts the whole host")
+
+
+def cpu_config1():
+    """BASELINE configs[0]: the 64x64 3-conv net (conv3x3 3->32 + ReLU, conv3x3 32->32 + ReLU,
+    conv1x1 32->3 + sigmoid), batch 1, fwd+bwd on the CPU oracle, repeated for ~2 s."""
+    from oracle import unet_ref as R
+    rng = np.random.default_rng(0)
+    P = R.init_tiny_params(0, np.float32)
+    x = (rng.integers(0, 256, size=(1, 64, 64, 3)) / 255.0).astype(np.float32)
+    t = (rng.integers(0, 256, size=(1, 64, 64, 3)) / 255.0).astype(np.float32)
+    net = R.TinyNetRef(P, np.float32)
+    net.forward(x)
+    net.backward(t)
+    k, t0 = 0, time.perf_counter()
+    while True:
+        net.forward(x)
+        net.backward(t)
+        k += 1
+        dt = time.perf_counter() - t0
+        if dt > 2.0:
+            break
+    cores, blas, model = _host_info()
+    return {"value": k / dt, "unit": "steps/s (64x64 patch, batch 1, fwd+bwd, fp32)", "cores": blas, "kind": "port",
+            "sample": f"oracle/unet_ref.py TinyNetRef, {k} steps in {dt:.2f} s", "ms_per_step": 1e3 * dt / k,
+            "gflop_per_step": round(3 * 2 * 64 * 64 * (27 * 32 + 288 * 32 + 32 * 3) / 1e9, 4)}
 
 
 # ---------------------------------------------------------------- launcher
@@ -278,23 +313,47 @@ def _spawn_ranks(args):
 
 
 # ---------------------------------------------------------------- legs
-def _roofline(agg, steps, elapsed, peak):
+def _lib_sha():
+    import hashlib
+    from cnn_itmo_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def _traffic(name, shape):
+    """HBM bytes per launch of kernel `name` from profiles/pmc_traffic.json (rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes, tools/pmc_traffic.sh) -> (bytes or None, provenance).
+    Reported only when that profile was taken of THIS library build at THIS shape."""
+    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if not os.path.exists(pmc):
+        return None, "no profiles/pmc_traffic.json"
+    try:
+        tab = json.load(open(pmc))
+    except Exception as e:  # pragma: no cover
+        return None, f"unreadable pmc_traffic.json: {e!r}"
+    meta = tab.get("_meta", {})
+    src = {"file": "profiles/pmc_traffic.json", "profile_lib_sha256": meta.get("lib_sha256"),
+           "profile_shapes": meta.get("shapes")}
+    ent = tab.get("per_shape", {}).get(shape, {}).get(name.split(" + ")[0])
+    if ent is None and shape in (meta.get("shapes") or []):
+        return None, dict(src, why_null="kernel not in the profile")
+    if meta.get("lib_sha256") != _lib_sha():
+        return None, dict(src, why_null="profile taken of another library build")
+    if shape not in (meta.get("shapes") or []):
+        return None, dict(src, why_null=f"profile shapes do not include {shape}")
+    return ent.get("bytes_per_launch"), src
+
+
+def _roofline(agg, steps, elapsed, peak, shape=None):
     dom = max(agg.items(), key=lambda kv: kv[1][2])
     name, (cnt, fl, ms, nbytes, nbcnt) = dom
     if nbcnt != cnt:  # bytes are accounted for the conv3x3 / tconv forwards only
         nbytes = 0
     achieved = fl / (ms * 1e-3) / 1e12
     step_flops = sum(v[1] for v in agg.values()) / steps
-    traffic = None
-    pmc = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            tab = json.load(open(pmc))
-            traffic = tab.get(name.split(" + ")[0], {}).get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, tsrc = _traffic(name, shape)
     return {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": traffic,
+            "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": tsrc,
             "launches": cnt, "avg_launch_ms": round(ms / cnt, 4),
             "algorithmic_flop_per_launch": fl / cnt,
             # single-pass HBM bytes (input, output, weights once) per launch, and the
@@ -408,7 +467,7 @@ def main():
 
     agg = timer.summary()
     peak = BF16_PEAK_TF if args.dtype == "bfloat16" else F32_PEAK_TF
-    roof, step_flops = _roofline(agg, k2, elapsed2, peak)
+    roof, step_flops = _roofline(agg, k2, elapsed2, peak, _shape(args.mode, args.height, args.width, B, args.dtype))
     roof["timed_pass_ms_per_step"] = round(elapsed2 / k2 * 1e3, 2)
     if rank == 0:
         _print_agg(agg, args.mode)
@@ -432,23 +491,40 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             cpu = cpu_baseline(args, P_init, H, W, train=args.mode == "train")
+            cpu["config1"] = cpu_config1()
         except Exception as e:  # report, never fail the bench on the CPU leg
             cpu = {"error": repr(e)}
 
+    # The secondary legs never cost the headline line: an exception (e.g. out of memory)
+    # is recorded in the leg's own field and the JSON line is still printed.
+    def guarded(fn, *a):
+        try:
+            return fn(*a)
+        except Exception as e:
+            import traceback
+            traceback.print_exc()
+            return {"error": repr(e)[:500]}
+        finally:
+            timer.on = False
+            timer.rec = []
+            C.clear_session()
+            torch.cuda.empty_cache()
+
     # configs[1]: fp32 inference leg (b8 1080p, BN moving stats), same ranks, weak
-    infer = k4 = None
-    if args.mode == "train" and (args.infer_batch > 0 or args.k4_batch > 0):
+    infer = ns = k4 = None
+    if args.mode == "train" and (args.infer_batch > 0 or args.k4_batch > 0 or args.ns_batch > 0):
         del eng, model, x, t, losses
         timer.rec = []
         C.clear_session()
         torch.cuda.empty_cache()
     if args.mode == "train" and args.infer_batch > 0:
-        infer = infer_leg(args, rank, world, timer, barrier, P_init, H, W)
-        C.clear_session()
-        torch.cuda.empty_cache()
+        infer = guarded(infer_leg, args, rank, world, timer, barrier, P_init, H, W, args.infer_batch, True)
+    # north star: fp32 conv2d forward at 1080p batch 32 (BASELINE.json "Target: >=40% of fp32 MFMA peak")
+    if args.mode == "train" and args.ns_batch > 0:
+        ns = guarded(infer_leg, args, rank, world, timer, barrier, P_init, H, W, args.ns_batch, False)
     # configs[4]: 4K training (b8 per GPU = global 64 on 8 GPUs), DP when N > 1
     if args.mode == "train" and args.k4_batch > 0:
-        k4 = k4_leg(args, rank, world, barrier)
+        k4 = guarded(k4_leg, args, rank, world, barrier)
 
     if rank == 0:
         res = "1080p" if (args.height, args.width) == (1080, 1920) else f"{args.width}x{args.height}"
@@ -469,6 +545,8 @@ def main():
             line["replicas"] = replicas
         if infer is not None:
             line["fp32_infer"] = infer
+        if ns is not None:
+            line["fp32_infer_b32"] = ns
         if k4 is not None:
             line["k4_train"] = k4
         print(json.dumps(line), flush=True)
@@ -476,11 +554,12 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def infer_leg(args, rank, world, timer, barrier, P_init, H, W):
-    """BASELINE configs[1]: 1080p frames, batch 8 per GPU, fp32, forward-only inference
+def infer_leg(args, rank, world, timer, barrier, P_init, H, W, B, with_cpu):
+    """BASELINE configs[1]: 1080p frames, batch B (8) per GPU, fp32, forward-only inference
     (predict.py:62 semantics: BN moving stats), through Model.predict's engine path with
     inputs resident in HBM.  Its own roofline (dominant kernel, HIP events) and CPU
-    baseline (the oracle's fp32 forward)."""
+    baseline (the oracle's fp32 forward).  With B = 32 it is the north star's
+    "fp32 conv2d fwd at 1080p batch=32" point."""
     import torch
     import cnn_itmo_amd as C
     with contextlib.redirect_stdout(io.StringIO()):
@@ -496,7 +575,7 @@ def infer_leg(args, rank, world, timer, barrier, P_init, H, W):
     m.set_named_weights(named)
     P = m.named_weights() if rank == 0 else None
     eng = m._engine()
-    B = args.infer_batch
+    torch.cuda.reset_peak_memory_stats()
     g = torch.Generator(device="cuda")
     g.manual_seed(77 + 7919 * rank)
     x = torch.randint(0, 256, (B, args.height, args.width, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
@@ -518,9 +597,9 @@ def infer_leg(args, rank, world, timer, barrier, P_init, H, W):
             torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
         return el.item()
 
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, min(args.warmup, 3) if B > 8 else args.warmup)):
         step()
-    k = max(args.steps, 5)
+    k = max(args.steps, 5) if B <= 8 else max(3, min(args.steps, 5))
     elapsed = timed(k)
     timer.reset()
     timer.on = True
@@ -528,23 +607,34 @@ def infer_leg(args, rank, world, timer, barrier, P_init, H, W):
     elapsed2 = timed(k2)
     timer.on = False
     agg = timer.summary()
-    roof, step_flops = _roofline(agg, k2, elapsed2, F32_PEAK_TF)
+    roof, step_flops = _roofline(agg, k2, elapsed2, F32_PEAK_TF, _shape("infer", args.height, args.width, B, "float32"))
     roof["timed_pass_ms_per_step"] = round(elapsed2 / k2 * 1e3, 2)
+    # the whole forward's conv FLOPs over its conv time: the north star's "% of fp32 MFMA peak on conv2d fwd"
+    conv_ms = sum(v[2] for v in agg.values()) / k2
+    roof["conv_fwd_tflops_all_layers"] = round(step_flops / (conv_ms * 1e-3) / 1e12, 2)
+    roof["conv_fwd_frac_all_layers"] = round(step_flops / (conv_ms * 1e-3) / 1e12 / F32_PEAK_TF, 4)
+    what = "BASELINE configs[1]" if B == 8 else "north star: fp32 conv2d fwd at 1080p batch 32"
     out = {"metric": "1080p SDR->HDR frames/sec (fwd, inference)", "value": round(B * world * k / elapsed, 3),
            "unit": "frames/s", "dtype": "f32", "steps": k, "ms_per_step": round(elapsed / k * 1e3, 2),
+           "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
            "config": {"workload": f"U-Net inference forward, {args.width}x{args.height} frames padded to "
-                                  f"{W}x{H}, {B} frames/GPU (BASELINE configs[1])", "global_batch": B * world,
+                                  f"{W}x{H}, {B} frames/GPU ({what})", "global_batch": B * world,
                       "gflop_per_frame": round(step_flops / B / 1e9, 1)},
            "roofline": roof, "cpu_baseline": None}
     if rank == 0:
-        _print_agg(agg, "infer")
-        if world == 1 and not args.no_cpu:
+        _print_agg(agg, f"infer b{B}")
+        if world == 1 and not args.no_cpu and with_cpu:
             try:
                 out["cpu_baseline"] = cpu_baseline(args, P, H, W, train=False)
             except Exception as e:
                 out["cpu_baseline"] = {"error": repr(e)}
     del eng, m, x, yhat
     return out
+
+
+def _shape(mode, h, w, b, dtype):
+    """Key of a profiled workload in profiles/pmc_traffic.json's _meta.shapes."""
+    return f"{mode} {h}x{w} b{b} {dtype}"
 
 
 def k4_leg(args, rank, world, barrier):

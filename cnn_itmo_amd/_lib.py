@@ -53,7 +53,7 @@ SIGNATURES = {
     "cnnitmo_im2col_c3": (i32, [i32, vp, i32, i32, i32, i32, vp, vp]),
     "cnnitmo_conv_c3_stat_rows": (i64, [i32, i32, i32]),
     "cnnitmo_bn_bwd_apply_g3": (i32, [i32, vp, vp, vp, i32, i32, i64, i32, vp, vp, vp, vp]),
-    "cnnitmo_head_fwd_bwd_g3": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "cnnitmo_head_fwd_bwd_g3": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, f64, vp]),
     "cnnitmo_conv_c3_fwd": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_conv_c3_wgrad_workspace_bytes": (sz, [i32, i32, i32]),
     "cnnitmo_conv_c3_wgrad": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, sz, vp]),
@@ -78,7 +78,7 @@ SIGNATURES = {
     "cnnitmo_colsum": (i32, [vp, i64, i32, i32, vp, vp, vp]),
     "cnnitmo_head_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_head_rows": (i32, [i64]),
-    "cnnitmo_head_fwd_bwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "cnnitmo_head_fwd_bwd": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, f64, vp]),
     "cnnitmo_head_finalize": (i32, [vp, i64, i32, f64, vp, vp, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_bn_consumer_sums": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
     "cnnitmo_pool_bnsums": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, i32, i32, vp, vp, vp, vp]),

@@ -106,6 +106,9 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the vmcnt switch
+#ifdef HALO_PRIO
+  if (wave >= NWAVE / 2) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
+#endif
   // logical id: contiguous per XCD (xcd_remap), so a stream's workgroups share one
   // XCD's L2 except where a stream straddles two XCDs
   const int lid = xcd_remap(blockIdx.x, gridDim.x);

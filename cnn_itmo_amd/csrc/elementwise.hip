@@ -1166,7 +1166,7 @@ extern "C" int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_va
 
 static int head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin, const float* wt,
                         const float* b, const float* scale, const float* shift, const float* target, void* dx,
-                        float* g3, float* part, void* stream) {
+                        float* g3, float* part, double grad_numel, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
   CNN_REQUIRE(cin % VE == 0 && (cin / VE) <= 64 && ((cin / VE) & (cin / VE - 1)) == 0,
@@ -1174,7 +1174,8 @@ static int head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int
   const long P = (long)n * h * w;
   CNN_REQUIRE(P < (1L << 31), "head: too many pixels");
   const int G = cnnitmo_head_rows(P);
-  const float inv_numel = (float)(1.0 / ((double)n * h_valid * w * 3));
+  const double numel = grad_numel > 0.0 ? grad_numel : (double)n * h_valid * w * 3;
+  const float inv_numel = (float)(1.0 / numel);
   if (launch_head2<true>(dtype, x, n, h, h_valid, w, cin, wt, b, target, nullptr, dx, inv_numel, part, scale,
                          shift, g3, G, s))
     return cnnitmo_check_launch("head_fwd_bwd");
@@ -1190,16 +1191,19 @@ static int head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int
 extern "C" int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w,
                                     int cin, const float* wt, const float* b, const float* scale,
                                     const float* shift, const float* target, void* dx, float* part,
-                                    void* stream) {
+                                    double grad_numel, void* stream) {
   CNN_REQUIRE(dx, "head_fwd_bwd: null dx");
-  return head_fwd_bwd(dtype, x, n, h, h_valid, w, cin, wt, b, scale, shift, target, dx, nullptr, part, stream);
+  return head_fwd_bwd(dtype, x, n, h, h_valid, w, cin, wt, b, scale, shift, target, dx, nullptr, part, grad_numel,
+                      stream);
 }
 
 extern "C" int cnnitmo_head_fwd_bwd_g3(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
                                        const float* wt, const float* b, const float* scale, const float* shift,
-                                       const float* target, float* g3, float* part, void* stream) {
+                                       const float* target, float* g3, float* part, double grad_numel,
+                                       void* stream) {
   CNN_REQUIRE(g3, "head_fwd_bwd_g3: null g3");
-  return head_fwd_bwd(dtype, x, n, h, h_valid, w, cin, wt, b, scale, shift, target, nullptr, g3, part, stream);
+  return head_fwd_bwd(dtype, x, n, h, h_valid, w, cin, wt, b, scale, shift, target, nullptr, g3, part, grad_numel,
+                      stream);
 }
 
 // Folded input BN (x = r, y = r*s + h): dW[o][c] = s[c]*sum(dz*r) + h[c]*db[o].

@@ -276,7 +276,10 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 #ifndef WH_ROWS96
 #define WH_ROWS96 2
 #endif
-constexpr int wh_rows(int bm, int bn) { return bm == 64 && bn == 96 ? WH_ROWS96 : 1; }
+#ifndef WH_ROWS_SMALL
+#define WH_ROWS_SMALL 1
+#endif
+constexpr int wh_rows(int bm, int bn) { return bm == 64 && bn == 96 ? WH_ROWS96 : WH_ROWS_SMALL; }
 
 struct WHPlan {
   int bm, bn, tw, strips, cbm, cbn, rsplits, smem;

@@ -165,6 +165,12 @@ class ImageDataGenerator:
         return ArrayIterator(x, y, self, batch_size, shuffle, seed, output, rank, world)
 
 
+# (tick, frames) of the latest global batch drawn by any rank-sharded iterator: lets
+# Model.fit_generator weight unequal shares exactly when the iterators reach it through
+# the reference's builtin ``zip(input, target)`` (main.py:99), which hides them.
+LAST_GLOBAL = [0, None]
+
+
 def _shard(rank, world):
     """(rank, world) for a generator: explicit values, else the initialised
     torch.distributed group, else (0, 1)."""
@@ -189,9 +195,12 @@ class Iterator:
     SAME stream for a global batch of ``batch_size * world`` frames -- the same
     reseeding, permutation and per-frame random transforms -- and keeps its
     contiguous share (``np.array_split`` of the global batch; a short last batch is
-    split as evenly as possible).  The union over ranks is therefore exactly the
-    single-process stream at the global batch size, and two generators with the same
-    seed stay paired on every rank (main.py:82-100's ``zip``)."""
+    split as evenly as possible, and one with fewer frames than ranks is dropped on
+    every rank -- no rank may get an empty batch).  The union over ranks is therefore
+    the single-process stream at the global batch size (less such a dropped tail), and
+    two generators with the same seed stay paired on every rank (main.py:82-100's
+    ``zip``).  ``last_global_batch`` is the frame count of the global batch last drawn:
+    Model.fit_generator normalises each rank's gradient by it (global-batch mean)."""
 
     def __init__(self, n, batch_size, shuffle, seed, rank=None, world=None):
         self.rank, self.world = _shard(rank, world)
@@ -203,6 +212,7 @@ class Iterator:
         self.global_batch = batch_size * self.world
         self.batch_index = 0
         self.total_batches_seen = 0
+        self.last_global_batch = None
         self.index_array = None
         self.rng = np.random.RandomState(seed)
         self._gen = self._flow_index()
@@ -235,16 +245,25 @@ class Iterator:
             else:
                 self.batch_index = 0
             self.total_batches_seen += 1
-            yield self.index_array[cur:cur + bs]
+            blk = self.index_array[cur:cur + bs]
+            if len(blk) < self.world:  # a tail too short to give every rank a frame
+                continue
+            yield blk
 
     def __len__(self):
-        return (self.n + self.global_batch - 1) // self.global_batch
+        full, tail = divmod(self.n, self.global_batch)
+        return full + (1 if tail >= self.world else 0)
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        return self._batch(next(self._gen))
+        blk = next(self._gen)
+        self.last_global_batch = len(blk)
+        if self.world > 1:
+            LAST_GLOBAL[0] += 1
+            LAST_GLOBAL[1] = len(blk)
+        return self._batch(blk)
 
     next = __next__
 

@@ -579,7 +579,8 @@ class HeadStage(Stage):
                 and prod.bn is not None and prod.drop is None and prod.kind == "c3"
                 and os.environ.get("CNNITMO_HEAD_G3", "1") != "0")
 
-    def loss_and_grad(self, n, target, loss_acc):
+    def loss_and_grad(self, n, target, loss_acc, grad_numel=0.0):
+        """grad_numel: the MSE gradient's normaliser (0: this batch's element count)."""
         e = self.eng
         P = n * self.vin.h * self.vin.w
         rows = ops.head_rows(P)
@@ -589,13 +590,13 @@ class HeadStage(Stage):
         if self._rank3():
             g3 = torch.empty(P * 3, device=e.device, dtype=torch.float32)
             ops.head_fwd_bwd_g3(e.dt, self.vin.view(n), e.h_valid, wt, e.p(self.name + "/bias"), target, g3,
-                                part, aff)
+                                part, aff, grad_numel)
             self.vin.grad_g3 = (g3, wt)
         else:
             self.vin.ensure_grad(n, e.tdtype, e.device)
             dx = self.vin.gview(n)
             ops.head_fwd_bwd(e.dt, self.vin.view(n), e.h_valid, wt, e.p(self.name + "/bias"), target, dx.buf,
-                             part, aff)
+                             part, aff, grad_numel)
         v = self.vin
         raw = torch.empty(3 * self.cin, device=e.device, dtype=torch.float32) \
             if e.training and v.sum_consumers and v.folded else None
@@ -896,15 +897,21 @@ class Engine:
         return yhat
 
     def train_step(self, x, target, seed=None, lr=1e-3, rho=0.9, eps=1e-7, grad_scale=1.0,
-                   sync=None, apply=True):
-        """One fwd+bwd+RMSprop step.  Returns a device tensor [loss, acc]."""
+                   sync=None, apply=True, grad_frames=None):
+        """One fwd+bwd+RMSprop step.  Returns a device tensor [loss, acc] (this batch's means).
+        grad_frames: the frame count the loss gradient is normalised by (default: this
+        batch's).  Data parallel with unequal shares, global_frames / world makes the
+        averaged gradient that of the global batch mean (Model.train_on_batch)."""
+        if x.shape[0] == 0:
+            raise ValueError("train_step: empty batch (BatchNormalization statistics of zero frames)")
         self.drop_seed = self.step if seed is None else int(seed)
         n = self.forward(x, training=True)
         if self.fwd_hook:
             self.fwd_hook()
         loss_acc = torch.empty(2, device=self.device, dtype=torch.float32)
         head = self.stages[-1]
-        head.loss_and_grad(n, target.contiguous().float(), loss_acc)
+        gn = 0.0 if grad_frames is None else float(grad_frames) * self.h_valid * self.model.inputs[0].shape[1] * 3
+        head.loss_and_grad(n, target.contiguous().float(), loss_acc, gn)
         if self.grad_hook:
             with self.side():  # hooks (DP all-reduce launches) follow both streams' writes
                 self.grad_hook(*self.stage_goff[-1])

@@ -254,11 +254,16 @@ class Model:
         if self.optimizer is None:
             raise RuntimeError("You must compile your model before using it.")
 
-    def train_on_batch(self, x, y, sync=True):
-        """One step on this rank's batch.  Distributed: the gradient is the mean over
-        ranks and every rank applies the same update; the returned loss/acc are this
-        rank's."""
+    def train_on_batch(self, x, y, sync=True, global_batch=None):
+        """One step on this rank's batch.  Distributed: every rank applies the same update,
+        the gradient of the GLOBAL batch mean when ``global_batch`` (the frames over all
+        ranks) is given -- each rank's loss gradient is normalised by global_batch/world
+        frames, so unequal shares are weighted by their size -- and otherwise the mean of
+        the ranks' batch-mean gradients.  The returned loss/acc are this rank's."""
         self._check_compiled()
+        if len(x) == 0:
+            raise ValueError("train_on_batch: empty batch (a data-parallel rank got no frames of a global batch "
+                             "smaller than the world size; such batches must be dropped on every rank)")
         eng = self._engine()
         o = self.optimizer
         kw = {}
@@ -266,6 +271,8 @@ class Model:
             r, w = self.world
             # per-rank dropout masks: seed = step*world + rank (one stream per replica)
             kw = dict(sync=self._dp.finish, grad_scale=self._dp.grad_scale, seed=eng.step * w + r)
+            if global_batch is not None:
+                kw["grad_frames"] = float(global_batch) / w
         la = eng.train_step(self._to_dev(x), self._to_dev(y), lr=o.lr, rho=o.rho, eps=o.epsilon, **kw)
         return la.cpu().numpy().tolist() if sync else la
 
@@ -283,8 +290,10 @@ class Model:
     def fit(self, x, y, batch_size=32, epochs=1, verbose=1, callbacks=None, shuffle=True, distributed=None,
             **kw):
         """keras Model.fit.  The permutation is drawn from numpy's global RNG each epoch
-        (as Keras does).  Distributed, ``batch_size`` is the GLOBAL batch: every rank
-        walks rank 0's permutation and trains on its contiguous share of each batch."""
+        (as Keras does).  Distributed, ``batch_size`` is PER RANK, as for the generators
+        (ImageDataGenerator.flow / flow_from_directory): every rank walks rank 0's
+        permutation in global batches of batch_size * world frames and trains on its
+        contiguous share; a global batch with fewer frames than ranks is dropped."""
         if distributed or (distributed is None and self._dp is None and _dist_world() > 1):
             self.distribute()
         r, w = self.world
@@ -298,14 +307,32 @@ class Model:
                 idx = box[0]
             return idx
 
-        def gen():
+        gb = batch_size * w
+
+        class _Gen:
+            last_global_batch = None
+
+            def __iter__(self):
+                return self
+
+            def __next__(self):
+                return next(it)
+
+        g = _Gen()
+
+        def batches():
             while True:
                 idx = perm()
-                for i in range(0, len(x), batch_size):
-                    j = np.array_split(idx[i:i + batch_size], w)[r]
+                for i in range(0, len(x), gb):
+                    blk = idx[i:i + gb]
+                    if len(blk) < w:
+                        continue
+                    g.last_global_batch = len(blk)
+                    j = np.array_split(blk, w)[r]
                     yield x[j], y[j]
-        steps = -(-len(x) // batch_size)
-        return self.fit_generator(gen(), steps_per_epoch=steps, epochs=epochs, verbose=verbose,
+        it = batches()
+        steps = sum(1 for i in range(0, len(x), gb) if len(x) - i >= w)
+        return self.fit_generator(g, steps_per_epoch=steps, epochs=epochs, verbose=verbose,
                                   callbacks=callbacks)
 
     def fit_generator(self, generator, steps_per_epoch=None, epochs=1, verbose=1, callbacks=None,
@@ -314,7 +341,9 @@ class Model:
         """keras Model.fit_generator (main.py:126-132): generator yields (x, y) batches.
 
         Epoch loss/acc are means over samples (per-step values weighted by batch size,
-        as Keras does).  ``distributed=True`` (or None with an initialised process group
+        as Keras does).  A generator exposing ``last_global_batch`` (the rank-sharded
+        ImageDataGenerator iterators, or a ``zip`` of two of them) gets global-batch-mean
+        gradients under data parallelism (see train_on_batch).  ``distributed=True`` (or None with an initialised process group
         of more than one rank) trains data-parallel: each rank consumes its own
         generator, logs are averaged over all ranks' samples, callbacks run on rank 0
         only and a ``stop_training`` raised there stops every rank."""
@@ -332,9 +361,11 @@ class Model:
             t0 = time.time()
             pending = []
             for step in range(steps_per_epoch):
+                from .datagen import LAST_GLOBAL
+                tick = LAST_GLOBAL[0]
                 xb, yb = next(generator)
                 cbs.call("on_batch_begin", step, {"batch": step, "size": len(xb)})
-                la = self.train_on_batch(xb, yb, sync=False)
+                la = self.train_on_batch(xb, yb, sync=False, global_batch=_global_batch(generator, tick))
                 pending.append((la, len(xb)))
                 cbs.call("on_batch_end", step, {"batch": step, "size": len(xb)})
             tot = np.zeros(3)
@@ -462,6 +493,18 @@ class Model:
             return
         with np.load(path, allow_pickle=False) as z:
             self.set_named_weights({k[2:]: z[k] for k in z.files if k.startswith("w/")})
+
+
+def _global_batch(gen, tick):
+    """Frames of the global batch just drawn over all ranks: the generator's own
+    ``last_global_batch`` (rank-sharded iterators, Model.fit), else the one recorded by
+    the rank-sharded iterators during this draw (the reference's builtin
+    ``zip(input, target)``, main.py:99, hides them); None if unknown."""
+    v = getattr(gen, "last_global_batch", None)
+    if v is not None:
+        return v
+    from .datagen import LAST_GLOBAL
+    return LAST_GLOBAL[1] if LAST_GLOBAL[0] != tick else None
 
 
 def _dist_world():

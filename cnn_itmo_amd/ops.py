@@ -280,17 +280,18 @@ def head_fwd(dt, x: View, h_valid, wt, b, yhat, aff=None):
          ptr(sh), ptr(yhat), stream_ptr())
 
 
-def head_fwd_bwd(dt, x: View, h_valid, wt, b, target, dx, part, aff=None):
+def head_fwd_bwd(dt, x: View, h_valid, wt, b, target, dx, part, aff=None, grad_numel=0.0):
+    """grad_numel: the MSE gradient's normaliser (0: this batch's element count; see cnn_itmo.h)."""
     sc, sh = aff if aff is not None else (None, None)
     call("cnnitmo_head_fwd_bwd", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b), ptr(sc),
-         ptr(sh), ptr(target), ptr(dx), ptr(part), stream_ptr())
+         ptr(sh), ptr(target), ptr(dx), ptr(part), float(grad_numel), stream_ptr())
 
 
-def head_fwd_bwd_g3(dt, x: View, h_valid, wt, b, target, g3, part, aff=None):
+def head_fwd_bwd_g3(dt, x: View, h_valid, wt, b, target, g3, part, aff=None, grad_numel=0.0):
     """head_fwd_bwd whose input gradient leaves as g3 [p][3] (dx = g3 . W)."""
     sc, sh = aff if aff is not None else (None, None)
     call("cnnitmo_head_fwd_bwd_g3", dt, x.ptr, x.n, x.h, h_valid, x.w, x.c, ptr(wt), ptr(b), ptr(sc),
-         ptr(sh), ptr(target), ptr(g3), ptr(part), stream_ptr())
+         ptr(sh), ptr(target), ptr(g3), ptr(part), float(grad_numel), stream_ptr())
 
 
 def bn_bwd_apply_g3(dt, g3, wh, r, c, p, coef, dz, part):

@@ -325,7 +325,12 @@ int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* ou
  * fwd: yhat [n,h,w,3] fp32 for rows < h_valid (predict.py:62).
  * fwd_bwd: target [n,h_valid,w,3] fp32; writes dx [p][cin] dtype
  * (= dz * W), and partials (loss sum, correct count, dW, db) into part;
- * cnnitmo_head_finalize reduces them into loss, acc, dw, db. */
+ * cnnitmo_head_finalize reduces them into loss, acc, dw, db.
+ * grad_numel: the element count the MSE gradient is normalised by (<= 0: this
+ * batch's n*h_valid*w*3, i.e. the gradient of its mean).  Data parallel with
+ * unequal shares: global_frames*h_valid*w*3/world, so that the all-reduced mean
+ * of the ranks' gradients is the gradient of the GLOBAL batch mean (the loss
+ * partials are unaffected). */
 int cnnitmo_head_fwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
                      const float* wt, const float* b, const float* scale, const float* shift,
                      float* yhat, void* stream);
@@ -333,12 +338,12 @@ int cnnitmo_head_rows(long p);
 int cnnitmo_head_fwd_bwd(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
                          const float* wt, const float* b, const float* scale,
                          const float* shift, const float* target, void* dx, float* part,
-                         void* stream);
+                         double grad_numel, void* stream);
 /* As cnnitmo_head_fwd_bwd, but the input gradient leaves as its rank-3 factor
  * g3 [p][3] fp32 = dL/dz of the head (dx = g3 * W; see cnnitmo_bn_bwd_apply_g3). */
 int cnnitmo_head_fwd_bwd_g3(int dtype, const void* x, int n, int h, int h_valid, int w, int cin,
                             const float* wt, const float* b, const float* scale, const float* shift,
-                            const float* target, float* g3, float* part, void* stream);
+                            const float* target, float* g3, float* part, double grad_numel, void* stream);
 int cnnitmo_head_finalize(const float* part, long rows, int cin, double numel,
                           const float* scale, const float* shift, float* loss_acc, float* dw,
                           float* db, float* raw_out, void* workspace, void* stream);

@@ -1,12 +1,12 @@
 """Per-launch checker for full-size runs (test infrastructure, GPU only).
 
-``LaunchChecker(ops, dt)`` wraps the conv / transposed-conv entry points of
+``LaunchChecker(ops, dt)`` wraps EVERY launching entry point of
 ``cnn_itmo_amd.ops`` so that, while the REAL engine runs a training step or an
 inference forward at a benchmarked shape (BASELINE configs[1], [2], [4]), every
 launch is verified the moment it returns, from the very buffers it read.  Each
 check restates the entry point's contract in include/cnn_itmo.h and evaluates
-it EXACTLY (fp64 on the GPU, torch GEMMs per image and tap -- an independent
-vendor path) over the WHOLE output:
+it EXACTLY (fp64 on the GPU; torch GEMMs per image and tap for the convolutions
+-- an independent vendor path) over the WHOLE output of the launch:
 
 * conv3x3 / tconv2x2 / first-layer forwards: bias, folded-BN border correction,
   ReLU, inference affine; their BN partial sums (STATS) against the exact
@@ -14,12 +14,20 @@ vendor path) over the WHOLE output:
 * input gradients, incl. the fused ``*_dgrad_bn`` launches' producer BN backward
   dz = [r>0]*(a*bf16(g) - b*r + e) and their column partials;
 * weight gradients, incl. the folded-BN correction (the reference differentiates
-  w.r.t. the conv's true input y = r*s + h) and the raw (uncorrected) sums.
+  w.r.t. the conv's true input y = r*s + h) and the raw (uncorrected) sums;
+* every launch that is not a GEMM (pooling, BatchNormalization forward and
+  backward in all their forms, Dropout, the sigmoid/MSE/accuracy head, RMSprop,
+  weight preparation and BN folding): ``launch_check_elem.py``.
+
+Coverage is enforced, not assumed: the checker also wraps ``ops.call`` and
+records any library call made outside a checked entry point
+(``LaunchChecker.unchecked``); the tests assert that set is empty.
 
 Tolerances: bf16 stores within 1.01*2^-8*|exact| + 2^-12*max|exact| (round-to-nearest
 of an fp32 accumulation); fp32 stores within 1e-5*|exact| + 1e-6*max|exact| + 8*2^-24*sqrt(K)*sum|w*x|;
 partial sums within 1e-5 of the channel's sum of |values|; weight gradients
-rel-L2 <= 1e-3 (bf16 inputs) / 1e-5 (fp32).
+rel-L2 <= 1e-3 (bf16 inputs) / 1e-5 (fp32); the non-GEMM checks state theirs in
+launch_check_elem.py.
 """
 from __future__ import annotations
 
@@ -28,6 +36,7 @@ import time
 import torch
 
 from cnn_itmo_amd import _lib as L
+from launch_check_elem import ElementwiseChecks
 
 F64 = torch.float64
 BF = torch.bfloat16
@@ -90,8 +99,9 @@ def _f32_slack(dt, K, absconv):
 class _Acc:
     """Streams per-image comparisons of one launch into one worst-case figure."""
 
-    def __init__(self, chk, label):
+    def __init__(self, chk, label, dt=None):
         self.chk, self.label = chk, label
+        self.dt = chk.dt if dt is None else dt
         self.pairs = []
 
     def add(self, got, ref, extra=None):
@@ -102,7 +112,7 @@ class _Acc:
         scale = max(scale, 1e-30)
         worst, maxerr = 0.0, 0.0
         for got, ref, extra in self.pairs:
-            if self.chk.dt == L.BF16:
+            if self.dt == L.BF16:
                 bound = 2.0 ** -8 * 1.01 * ref.abs() + 2.0 ** -12 * scale
             else:
                 bound = 1e-5 * ref.abs() + 1e-6 * scale
@@ -115,30 +125,64 @@ class _Acc:
         assert worst <= 1.0, f"{self.label}: max |got-exact|/bound = {worst:.3f} (max err {maxerr:.3e}, scale {scale:.3e})"
 
 
-class LaunchChecker:
+# every launching entry point of cnn_itmo_amd.ops (all of them go through ops.call)
+LAUNCHES = ("conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
+            "conv_wgrad", "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad", "conv1tap_fwd", "im2col_c3",
+            "maxpool_fwd", "maxpool_bwd", "pool_bnsums", "bn_fwd_finalize", "bn_infer_coeffs", "bn_apply",
+            "bn_bwd_reduce", "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3",
+            "bn_consumer_sums", "colsum", "border_sums", "head_fwd", "head_fwd_bwd", "head_fwd_bwd_g3",
+            "head_finalize", "rmsprop", "prep_conv3x3", "prep_tconv", "prep_c3", "fold_conv3x3", "fold_tconv")
+
+
+class LaunchChecker(ElementwiseChecks):
     def __init__(self, ops, dt, verbose=True):
         self.ops, self.dt, self.verbose = ops, dt, verbose
         self.log = []   # (launch label, metric, value)
         self.orig = {}
-        names = ("conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
-                 "conv_wgrad", "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad", "conv1tap_fwd", "im2col_c3")
-        for nm in names:
+        self.calls = {}  # entry point -> checked launches
+        self.unchecked = {}  # library symbol -> calls made outside a checked entry point
+        self._depth = 0
+        for nm in LAUNCHES:
             self.orig[nm] = getattr(ops, nm)
             setattr(ops, nm, self._wrap(nm))
+        self.orig["call"] = ops.call
+        lib_call = ops.call
+
+        def call(name, *a):
+            if self._depth == 0:
+                self.unchecked[name] = self.unchecked.get(name, 0) + 1
+            return lib_call(name, *a)
+        ops.call = call
 
     def restore(self):
         for nm, f in self.orig.items():
             setattr(self.ops, nm, f)
 
+    def _acc(self, label, dt=None):
+        return _Acc(self, label, dt)
+
     def _wrap(self, nm):
         orig, chk = self.orig[nm], getattr(self, "_chk_" + nm)
+        pre = getattr(self, "_pre_" + nm, None)
 
         def f(*a, **k):
-            r = orig(*a, **k)
+            snap = None
+            if pre is not None:  # in-place operands: their state before the launch
+                torch.cuda.synchronize()
+                snap = pre(*a, **k)
+            self._depth += 1
+            try:
+                r = orig(*a, **k)
+            finally:
+                self._depth -= 1
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             n0 = len(self.log)
-            chk(*a, **k)
+            if pre is not None:
+                chk(*a, pre=snap, **k)
+            else:
+                chk(*a, **k)
+            self.calls[nm] = self.calls.get(nm, 0) + 1
             if self.verbose:  # progress: one line per checked launch
                 worst = ", ".join(f"{m} {v:.2e}" for _, m, v in self.log[n0:])
                 lab = self.log[n0][0] if len(self.log) > n0 else nm

@@ -163,32 +163,39 @@ def test_gpu_paired_generators_feed_fit_generator(tmp_path):
 def test_rank_shards_union_is_global_stream(world, nfr, bs):
     """8e / 8f row 3: each rank's stream (batch bs) is its contiguous share of the
     single-process stream at batch bs*world -- same frames, same random transforms,
-    ragged last batches split as evenly as possible."""
+    ragged last batches split as evenly as possible, and a tail with fewer frames
+    than ranks (world 4, 9 frames: 8 + 1) dropped on every rank, never an empty share."""
     rng = np.random.default_rng(1)
     frames = rng.integers(0, 256, (nfr, 8, 8, 3), dtype=np.uint8)
     nb = 7
     g = D.ImageDataGenerator(**REF_ARGS)
     cap = _Capture(g)
     it = g.flow(frames, batch_size=bs * world, seed=5, world=1)
-    for _ in range(nb):
+    ref, gsz = [], []
+    while len(ref) < nb:
         next(it)
+        if len(cap.seen[-1][0]) >= world:
+            ref.append(cap.seen[-1])
+            gsz.append(len(cap.seen[-1][0]))
     shards = []
     for r in range(world):
         gr = D.ImageDataGenerator(**REF_ARGS)
         cr = _Capture(gr)
         itr = gr.flow(frames, batch_size=bs, seed=5, rank=r, world=world)
-        assert len(itr) == len(it)
-        for _ in range(nb):
+        assert len(itr) == nfr // (bs * world) + (1 if nfr % (bs * world) >= world else 0)
+        for b in range(nb):
+            tick = D.LAST_GLOBAL[0]
             next(itr)
+            assert itr.last_global_batch == gsz[b] and D.LAST_GLOBAL == [tick + 1, gsz[b]]
         shards.append(cr.seen)
     for b in range(nb):
-        fr, params = cap.seen[b]
+        fr, params = ref[b]
         got_fr = np.concatenate([shards[r][b][0] for r in range(world)])
         got_p = sum((shards[r][b][1] for r in range(world)), [])
         np.testing.assert_array_equal(got_fr, fr)
         assert got_p == params
         sizes = [len(shards[r][b][0]) for r in range(world)]
-        assert max(sizes) - min(sizes) <= 1
+        assert max(sizes) - min(sizes) <= 1 and min(sizes) >= 1
 
 
 def test_rank_shards_stay_paired_and_validate():

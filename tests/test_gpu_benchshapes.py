@@ -1,14 +1,17 @@
 """Parity at the benchmarked shapes (BASELINE configs[1], [2], [4]): the real
 engine runs one step of each benchmarked workload -- the same model, dtype,
-batch and frame as bench.py -- with every conv / transposed-conv launch checked
-the moment it returns (tests/launch_check.py: sampled fp64 dot products for the
-forward and input-gradient launches incl. the fused BN-backward stores, whole
-fp64 reductions for the weight gradients).  This pins the persistent grids,
-960-column partial strips, 2-GB buffer-descriptor rebasing and 2^31 guards that
-only exist at these sizes.
+batch and frame as bench.py -- with EVERY launch checked the moment it returns
+against an fp64 restatement of its contract over its whole output
+(tests/launch_check.py for the convolutions, tests/launch_check_elem.py for
+pooling, BatchNormalization, Dropout, the head, RMSprop, weight preparation and
+BN folding).  Library calls outside a checked entry point fail the test.  This
+pins the persistent grids, 960-column partial strips, 2-GB buffer-descriptor
+rebasing and 2^31 guards that only exist at these sizes.
 
   configs[2]  1920x1080 (padded 1088), batch 32, bf16 training step
   configs[1]  1920x1080 (padded 1088), batch 8, fp32 inference (BN moving stats)
+  north star  1920x1080 (padded 1088), batch 32, fp32 inference: the conv2d-forward
+              point of BASELINE.json's target (fp32 buffers of 6.4 G elements)
   configs[4]  3840x2160, batch 8 per GPU, bf16 training step (no padding)
 """
 import contextlib
@@ -62,27 +65,44 @@ def _run(h, w, batch, dtype, train, expect):
     summ = chk.summary()
     for (lab, met), v in sorted(summ.items()):
         print(f"{lab:60s} {met:14s} {v:.3e}")
-    kinds = {lab.split(" ")[0] for lab, _ in summ}
-    missing = set(expect) - kinds
-    assert not missing, f"launch kinds never checked: {missing}"
+    print("checked launches per entry point:", dict(sorted(chk.calls.items())))
+    assert not chk.unchecked, f"library calls outside a checked entry point: {chk.unchecked}"
+    missing = set(expect) - set(chk.calls)
+    assert not missing, f"entry points never launched/checked: {missing}"
+
+
+TRAIN = ["conv_c3_fwd", "conv3x3_fwd", "tconv_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_dgrad",
+         "tconv_dgrad_bn", "conv_wgrad", "tconv_wgrad", "conv_c3_wgrad",
+         "maxpool_fwd", "maxpool_bwd", "pool_bnsums", "bn_fwd_finalize", "bn_apply", "bn_bwd_reduce",
+         "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3", "bn_consumer_sums", "colsum",
+         "border_sums", "head_fwd_bwd_g3", "head_finalize", "rmsprop", "prep_conv3x3", "prep_tconv", "prep_c3",
+         "fold_conv3x3", "fold_tconv"]
+INFER_F32 = ["prep_conv3x3", "prep_tconv", "prep_c3", "im2col_c3", "conv1tap_fwd", "conv3x3_fwd", "tconv_fwd",
+             "maxpool_fwd", "bn_infer_coeffs", "head_fwd"]
 
 
 def test_config2_train_1080p_b32_bf16():
-    _run(1080, 1920, 32, "bfloat16", True,
-         ["conv_c3_fwd", "conv3x3_fwd", "tconv_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_dgrad",
-          "tconv_dgrad_bn", "conv_wgrad(9)", "tconv_wgrad", "conv_c3_wgrad"])
+    _run(1080, 1920, 32, "bfloat16", True, TRAIN)
 
 
 def test_config1_infer_1080p_b8_f32():
-    _run(1080, 1920, 8, "float32", False, ["im2col_c3", "conv1tap_fwd", "conv3x3_fwd", "tconv_fwd"])
+    _run(1080, 1920, 8, "float32", False, INFER_F32)
+
+
+@pytest.mark.timeout(900)
+def test_northstar_infer_1080p_b32_f32():
+    """BASELINE.json's north-star point: fp32 conv2d forward at 1080p batch 32."""
+    _run(1080, 1920, 32, "float32", False, INFER_F32)
 
 
 def test_config4_train_4k_b8_bf16():
-    _run(2160, 3840, 8, "bfloat16", True,
-         ["conv_c3_fwd", "conv3x3_fwd", "tconv_fwd", "conv3x3_dgrad_bn", "conv_wgrad(9)", "tconv_wgrad"])
+    _run(2160, 3840, 8, "bfloat16", True, TRAIN)
 
 
 @pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
 def test_small_frame_all_launch_kinds(dtype):
     """The same per-launch checks on a small ragged frame (quick; every kind)."""
-    _run(72, 112, 2, dtype, True, ["conv3x3_fwd", "tconv_fwd", "conv_wgrad(9)", "tconv_wgrad"])
+    # fp32 training runs the unfused BN backward (no *_dgrad_bn) and the im2col first layer
+    exp = TRAIN if dtype == "bfloat16" else [k for k in TRAIN if not k.startswith("conv_c3") and "dgrad_bn" not in k] \
+        + ["im2col_c3", "conv1tap_fwd"]
+    _run(72, 112, 2, dtype, True, exp)

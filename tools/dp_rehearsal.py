@@ -10,8 +10,9 @@ Checks (rank 0):
   * they equal a single-process replay that draws the UNSHARDED stream at the
     global batch size (batch * world), splits each global batch into the ranks'
     shares, runs each share with that rank's dropout seed from the same starting
-    state, averages the gradients and the moving statistics itself and applies
-    RMSprop once;
+    state, weights each share's batch-mean gradient by its share of the global batch
+    (the 11-frame stream ends in a 3-frame global batch: shares 2 and 1), averages
+    the moving statistics itself and applies RMSprop once;
   * the epoch loss equals the sample-weighted mean of the replay's per-share losses.
 
   CNNITMO_DEVICE=0 CNNITMO_DIST_BACKEND=gloo python -m torch.distributed.run \\
@@ -90,11 +91,11 @@ def main():
                 la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False)
                 lsum += float(la[0]) * len(ix)
                 nsum += len(ix)
-                acc += e2.grads
+                acc += e2.grads * (len(ix) / len(xb))  # the global batch mean's gradient
                 bacc += e2.bufs
             e2.step -= world - 1
             e2.bufs.copy_(bacc * (1.0 / world))
-            ops.rmsprop(e2.params, acc, e2.accum, 1e-3, 0.9, 1e-7, 1.0 / world)
+            ops.rmsprop(e2.params, acc, e2.accum, 1e-3, 0.9, 1e-7, 1.0)
             e2.weights_dirty = True
         torch.cuda.synchronize()
         q = e2.params.cpu().numpy()

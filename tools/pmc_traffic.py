@@ -1,5 +1,8 @@
-"""HBM bytes per launch per kernel from the two rocprofv3 --pmc passes of
-tools/pmc_traffic.sh -> profiles/pmc_traffic.json (read by bench.py's roofline).
+"""HBM bytes per launch per kernel from the rocprofv3 --pmc passes of
+tools/pmc_traffic.sh (two per workload shape) -> profiles/pmc_traffic.json (read by
+bench.py's roofline, which uses it only for the same library build and shape).
+
+    python tools/pmc_traffic.py gpurun_out profiles/pmc_traffic.json
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 128-B
 requests at 64 B, i.e. half the bytes of wide coalesced reads -> doubled;
@@ -83,7 +86,7 @@ def load(path):
     return per, kern
 
 
-def main(fetch_csv, write_csv, out_json):
+def table(fetch_csv, write_csv):
     f, kf = load(fetch_csv)
     w, kw = load(write_csv)
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0])
@@ -96,12 +99,30 @@ def main(fetch_csv, write_csv, out_json):
     for k, (n, rd, wr) in sorted(agg.items(), key=lambda kv: -(kv[1][1] + kv[1][2])):
         res[k] = {"launches": n, "read_bytes_per_launch": rd / n, "write_bytes_per_launch": wr / max(n, 1),
                   "bytes_per_launch": (rd + wr) / n}
-    meta = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 1",
-            "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); KiB -> bytes"}
-    json.dump({"_meta": meta, **res}, open(out_json, "w"), indent=1)
-    for k, v in list(res.items())[:15]:
-        print(f"{k:45s} {v['launches']:4d} {v['bytes_per_launch'] / 1e9:8.3f} GB/launch")
+    return res
+
+
+def main(outdir, out_json):
+    """outdir: gpurun_out/ of a tools/pmc_traffic.sh run (pmc_<SHAPE_TAG>_<COUNTER>/ + lib_sha.txt)."""
+    import glob
+    import os
+    shapes = {}
+    for tag_file in sorted(glob.glob(os.path.join(outdir, "pmc_*_FETCH_SIZE.shape"))):
+        tag = os.path.basename(tag_file)[len("pmc_"):-len("_FETCH_SIZE.shape")]
+        shape = open(tag_file).read().strip()
+        fc = glob.glob(os.path.join(outdir, f"pmc_{tag}_FETCH_SIZE", "**", "*counter_collection.csv"), recursive=True)
+        wc = glob.glob(os.path.join(outdir, f"pmc_{tag}_WRITE_SIZE", "**", "*counter_collection.csv"), recursive=True)
+        shapes[shape] = table(fc[0], wc[0])
+        print(shape)
+        for k, v in list(shapes[shape].items())[:12]:
+            print(f"  {k:45s} {v['launches']:4d} {v['bytes_per_launch'] / 1e9:8.3f} GB/launch")
+    meta = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), one bench.py step per shape "
+                      "(tools/pmc_traffic.sh)",
+            "correction": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); KiB -> bytes",
+            "lib_sha256": open(os.path.join(outdir, "pmc_lib_sha.txt")).read().strip(),
+            "shapes": sorted(shapes)}
+    json.dump({"_meta": meta, "per_shape": shapes}, open(out_json, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:3])
