@@ -111,7 +111,7 @@ class KernelTimer:
     def _wrap(self):
         ops = self.ops
         query = functools.lru_cache(maxsize=None)(ops.query)  # kernel names: one ctypes query per shape
-        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
+        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
                                            "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
                                            "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad")}
 
@@ -124,6 +124,21 @@ class KernelTimer:
             self._nb = (2 if dt == 1 else 4) * (x.p * x.c + x.p * out.c + 9 * x.c * out.c)
             return self._bracket(kname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, f"fwd {x.h}x{x.w} {x.c}->{out.c}", o["conv3x3_fwd"], dt, x, wt, bias,
                                  out, *a, **k)
+
+        def conv3x3_fwd_cat(dt, x1, x2, wt, bias, out, *a, **k):
+            cin = x1.c + x2.c
+            fl = 2.0 * x1.p * out.c * 9 * cin
+            self._nb = 2 * (x1.p * cin + x1.p * out.c + 9 * cin * out.c)
+            return self._bracket(kname(dt, x1.n, x1.h, x1.w, cin, out.c, 0), fl,
+                                 f"fwd {x1.h}x{x1.w} {x1.c}+{x2.c}->{out.c}", o["conv3x3_fwd_cat"], dt, x1, x2, wt, bias,
+                                 out, *a, **k)
+
+        def conv_wgrad_cat(dt, x1, x2, dz, cout, dw, *a, **k):
+            cin = x1.c + x2.c
+            fl = 2.0 * x1.p * cout * 9 * cin
+            name = query("cnnitmo_wgrad_cat_kernel_name", x1.n, x1.h, x1.w, x1.c, cin, cout).decode() + " + slab_reduce"
+            return self._bracket(name, fl, f"wgrad {x1.h}x{x1.w} {x1.c}+{x2.c}->{cout}", o["conv_wgrad_cat"], dt, x1, x2,
+                                 dz, cout, dw, *a, **k)
 
         def conv3x3_dgrad(dt, dz, n, h, w, cout, wflip, cin, dx):
             fl = 2.0 * n * h * w * cin * 9 * cout
@@ -181,7 +196,8 @@ class KernelTimer:
             return self._bracket(wname(dt, 4, x.n, x.h, x.w, x.c, cout), fl, f"t.wgrad {x.h}x{x.w} {x.c}->{cout}", o["tconv_wgrad"],
                                  dt, x, dout, cout, dk, *a, **k)
 
-        for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_dgrad", conv3x3_dgrad),
+        for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_fwd_cat", conv3x3_fwd_cat), ("conv_wgrad_cat", conv_wgrad_cat),
+                     ("conv3x3_dgrad", conv3x3_dgrad),
                      ("conv3x3_dgrad_bn", conv3x3_dgrad_bn), ("tconv_fwd", tconv_fwd),
                      ("tconv_dgrad", tconv_dgrad), ("tconv_dgrad_bn", tconv_dgrad_bn), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),
                      ("tconv_wgrad", tconv_wgrad), ("conv_c3_fwd", conv_c3_fwd), ("conv_c3_wgrad", conv_c3_wgrad)):

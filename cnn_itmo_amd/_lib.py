@@ -41,6 +41,12 @@ SIGNATURES = {
     "cnnitmo_tonemap_apply": (i32, [i32, vp, i32, i32, i32, vp, vp, vp, i32, vp, vp]),
     "cnnitmo_inverse_reinhard_apply": (i32, [i32, vp, i32, i32, i32, vp, vp, f64, f64, vp, vp]),
     "cnnitmo_conv3x3_fwd": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp, vp]),
+    "cnnitmo_conv3x3_fwd_cat": (i32, [i32, vp, i32, i32, i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32,
+                                      i32, i32, vp, vp, vp, vp, vp]),
+    "cnnitmo_wgrad_cat_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32]),
+    "cnnitmo_wgrad_cat_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32]),
+    "cnnitmo_conv_wgrad_cat": (i32, [i32, vp, i32, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, vp, vp, vp,
+                                     vp, vp, vp, vp, sz, vp]),
     "cnnitmo_fwd_stat_rows": (i32, [i32, i64, i32]),
     "cnnitmo_tconv2x2_dgrad_bn_rows": (i64, [i32, i32, i32, i32, i32, i32]),
     "cnnitmo_tconv2x2_dgrad_bn": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, vp, vp, vp]),

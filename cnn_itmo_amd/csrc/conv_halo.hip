@@ -64,6 +64,11 @@ constexpr int NPI = (PPC + NWAVE - 1) / NWAVE;                    // patch piece
 // taps over which the next item's DMA pieces are issued (3 and 8 measured no better,
 // profiles/r02l_ab_halo_knobs.txt)
 constexpr int PFT = 5;
+// tap offset of the DMA issue window for waves NWAVE/2.. (the second wave on each SIMD):
+// the two waves of a SIMD then issue their pieces in different taps
+#ifndef HALO_PFT_OFF
+#define HALO_PFT_OFF 0
+#endif
 
 // RES: the workgroup's weights for the whole K (at most RCH chunks) stay resident in
 // LDS, loaded once per launch; a ring stage then holds the halo patch only.  For the
@@ -172,7 +177,9 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // 4 pieces of 16 B; lane -> (row, piece), source piece swizzled
   const int lrow = lane >> 2, lpc = lane & 3;
   int ppy[NPI], ppx[NPI];
-  unsigned poff[NPI];  // byte offset of the lane's source piece from the patch origin
+  // EPI 1 (two-source capable): 4 * (source pixel offset from the patch origin) + swizzled
+  // piece, the row pitch chosen per chunk; otherwise the byte offset of the lane's piece
+  unsigned pkey[NPI];
 #pragma unroll
   for (int i = 0; i < NPI; ++i) {
     const int row = (wave * NPI + i) * 16 + lrow;
@@ -180,8 +187,12 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const int py = row / PW, px = row - (row / PW) * PW;
     ppy[i] = row < PROWS ? py - 1 : -(1 << 29);  // padding rows: never in bounds
     ppx[i] = px - 1;
-    poff[i] = (unsigned)((((long)py * p.ws + px) * p.a_ld + piece * 8) * 2);
+    pkey[i] = EPI == 1 ? (unsigned)((py * p.ws + px) * 4 + piece)
+                       : (unsigned)((((long)py * p.ws + px) * p.a_ld + piece * 8) * 2);
   }
+  // the source of a chunk: a (channels < cin1 or a single source) or a2
+  const bf16* __restrict__ X2 = (const bf16*)p.a2;
+  const int cin1 = p.a2 ? p.cin1 : p.cin;
   unsigned boff[NBI];
 #pragma unroll
   for (int i = 0; i < NBI; ++i) {
@@ -197,13 +208,27 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const Pos& s = ip;
     iPs = smem + buf * STAGE;
     const long po = ((long)s.img * p.hs + s.y0 - 1) * p.ws + s.x0 - 1;  // patch origin pixel (may be < 0)
-    pbase = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + s.ch * 32) * 2);
-    bbase = (uintptr_t)(Wt + (size_t)n0 * K + s.ch * 32);
+    const int c = s.ch * 32;
+    bbase = (uintptr_t)(Wt + (size_t)n0 * K + c);
+    if constexpr (EPI == 1) {
+      const bool second = c >= cin1;
+      const long ld = second ? p.a2_ld : p.a_ld;
+      pbase = second ? (uintptr_t)X2 + (uintptr_t)((po * ld + p.a2_off + c - cin1) * 2)
+                     : (uintptr_t)X + (uintptr_t)((po * ld + p.a_off + c) * 2);
 #pragma unroll
-    for (int i = 0; i < NPI; ++i) {
-      const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
-      const bool ok = (unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws;
-      pvo[i] = ok ? poff[i] : OOB;
+      for (int i = 0; i < NPI; ++i) {
+        const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
+        const bool ok = (unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws;
+        pvo[i] = ok ? ((pkey[i] >> 2) * (unsigned)ld + (pkey[i] & 3) * 8) * 2 : OOB;
+      }
+    } else {
+      pbase = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + c) * 2);
+#pragma unroll
+      for (int i = 0; i < NPI; ++i) {
+        const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
+        const bool ok = (unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws;
+        pvo[i] = ok ? pkey[i] : OOB;
+      }
     }
   };
   auto issue_piece = [&](int k) {  // k: compile-time after unrolling
@@ -275,9 +300,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], bfr[cur][j], af[cur][i]);  // C^T: lanes = pixels
       if (pf) {
+        const int toff = HALO_PFT_OFF && wave >= NWAVE / 2 ? HALO_PFT_OFF : 0;
 #pragma unroll
         for (int k = 0; k < L; ++k)
-          if ((k * PFT) / L == tap) issue_piece(k);
+          if ((k * PFT) / L + toff == tap) issue_piece(k);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -566,6 +592,8 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
   }();
   if (!en) return false;
   if (a.cin % 32 || a.a_ld % 8 || a.a_off % 8 || a.out_ld % 8 || a.out_off % 8) return false;
+  if (a.a2 && (a.cin1 % 32 || a.cin1 <= 0 || a.cin1 >= a.cin || a.a2_ld % 8 || a.a2_off % 8 || a.bnb_out))
+    return false;
   if (a.ntaps != 9 || a.scale != 1 || a.scatter || a.hs != a.ho || a.ws != a.wo) return false;
   pl.bn = a.N % 64 == 0 ? 64 : (a.N % 32 == 0 ? 32 : 0);
   if (!pl.bn || a.N / pl.bn > halo_ncu() / 8) return false;
@@ -576,6 +604,7 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
     pl.epi = 2;
   } else {
     pl.epi = (a.flags || a.bias || a.border || a.stats) ? 1 : 0;
+    if (a.a2 && pl.epi != 1) return false;  // two sources: the forward-epilogue kernels only
   }
   static const int res = [] {
     const char* e = getenv("CNNITMO_HALO_RES");

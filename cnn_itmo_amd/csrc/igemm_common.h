@@ -36,6 +36,13 @@ struct FwdArgs {
   long bnb_r_ld;
   int bnb_r_off;
   void* bnb_out;
+  // two-source input (a concatenate consumed without a concat buffer; halo kernel only):
+  // channels [0, cin1) come from a (a_ld, a_off), channels [cin1, cin) from a2 (channel
+  // c - cin1 at a2_ld, a2_off).  cin1 = 0: a single source.
+  const void* a2;
+  long a2_ld;
+  int a2_off;
+  int cin1;
 };
 
 // Out-of-bounds-tap correction for a folded BN shift (see cnnitmo_fold_conv3x3):
@@ -147,7 +154,9 @@ const char* wgrad_tconv_name(int n, int h, int w, int cin, int cout);
 int launch_wgrad_tconv(const bf16* x, long x_ld, int x_off, const bf16* dy, int n, int h, int w, int cin,
                        int cout, float* ws, size_t ws_bytes, hipStream_t s);
 // sliding-window bf16 3x3 weight gradient for the high-resolution layers, wgrad_halo.hip
-size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout);
-const char* wgrad_halo_name(int n, int h, int w, int cin, int cout);
+// (x2 != null: a concatenate's two members, channels [0, 32) from x and [32, cin) from x2)
+size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout, bool cat = false);
+const char* wgrad_halo_name(int n, int h, int w, int cin, int cout, bool cat = false);
 int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n, int h, int w, int cin,
-                      int cout, float* ws, size_t ws_bytes, hipStream_t s);
+                      int cout, float* ws, size_t ws_bytes, hipStream_t s, const bf16* x2 = nullptr,
+                      long x2_ld = 0, int x2_off = 0);

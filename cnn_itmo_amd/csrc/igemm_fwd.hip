@@ -374,6 +374,31 @@ extern "C" int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off
   return dispatch(dtype, a, stream, "conv3x3_fwd");
 }
 
+extern "C" int cnnitmo_conv3x3_fwd_cat(int dtype, const void* x1, int x1_ld, int x1_off, int c1, const void* x2,
+                                       int x2_ld, int x2_off, int n, int h, int w, int cin, const void* wt,
+                                       const float* bias, int cout, void* out, int out_ld, int out_off, int flags,
+                                       const float* aff_scale, const float* aff_shift, float* stat_part,
+                                       const float* border, void* stream) {
+  FwdArgs a = base_args();
+  a.a = x1; a.a_ld = x1_ld; a.a_off = x1_off;
+  a.a2 = x2; a.a2_ld = x2_ld; a.a2_off = x2_off; a.cin1 = c1;
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cin; a.b = wt; a.N = cout; a.M = (long)n * h * w;
+  a.bias = bias; a.out = out; a.out_ld = out_ld; a.out_off = out_off;
+  a.cout = cout; a.flags = flags; a.aff_scale = aff_scale; a.aff_shift = aff_shift;
+  a.stats = stat_part;
+  a.border = border;
+  CNN_REQUIRE(x1 && x2 && c1 > 0 && c1 < cin, "conv3x3_fwd_cat: needs two sources splitting cin");
+  CNN_REQUIRE(!(flags & CNNITMO_STATS) || stat_part, "conv3x3_fwd_cat: STATS without buffer");
+  CNN_REQUIRE(!(flags & CNNITMO_AFFINE) || (aff_scale && aff_shift), "conv3x3_fwd_cat: AFFINE without coefficients");
+  if (dtype != CNNITMO_BF16 || !halo_handles(a)) {
+    cnnitmo_set_error("conv3x3_fwd_cat: unsupported (bf16 halo kernel, 32-channel aligned split, with an epilogue)");
+    return CNNITMO_EUNSUPPORTED;
+  }
+  return launch_halo(a, (hipStream_t)stream, "conv3x3_fwd_cat");
+}
+
 // Name of the kernel cnnitmo_conv3x3_fwd (dgrad = 0) or cnnitmo_conv3x3_dgrad
 // (dgrad = 1; cin/cout as in the layer) launches for these sizes (for profiles).
 extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int w, int cin, int cout,

@@ -508,6 +508,36 @@ extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld,
   return CNNITMO_EUNSUPPORTED;
 }
 
+extern "C" size_t cnnitmo_wgrad_cat_workspace_bytes(int n, int h, int w, int c1, int cin, int cout) {
+  return c1 == 32 ? wgrad_halo_ws_bytes(n, h, w, cin, cout, true) : 0;
+}
+
+extern "C" int cnnitmo_conv_wgrad_cat(int dtype, const void* x1, int x1_ld, int x1_off, int c1, const void* x2,
+                                      int x2_ld, int x2_off, const void* dz, int n, int h, int w, int cin, int cout,
+                                      float* dw, const float* fold_scale, const float* fold_shift,
+                                      const float* fold_db, const float* fold_border, float* raw_out,
+                                      void* workspace, size_t ws_bytes, void* stream) {
+  CNN_REQUIRE(dtype == CNNITMO_BF16 && c1 == 32 && x1 && x2,
+              "conv_wgrad_cat: bf16 with a 32-channel first source only");
+  WFold f{0, cin, cout, fold_scale, fold_shift, fold_db, fold_border, raw_out};
+  if (fold_scale) {
+    CNN_REQUIRE(fold_shift && fold_db && fold_border, "conv_wgrad_cat: folded BN needs shift, db and border sums");
+    f.mode = 1;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int splits = launch_wgrad_halo((const bf16*)x1, x1_ld, x1_off, (const bf16*)dz, n, h, w, cin, cout,
+                                       (float*)workspace, ws_bytes, s, (const bf16*)x2, x2_ld, x2_off);
+  CNN_REQUIRE(splits > 0, "conv_wgrad_cat: unsupported sizes (%dx%d, %d+%d -> %d) or workspace too small", h, w,
+              c1, cin - c1, cout);
+  int rc = cnnitmo_check_launch("conv_wgrad_cat");
+  if (rc) return rc;
+  const long slab = (long)cout * 9 * cin;
+  const int rblocks = (int)std::min<long>((slab + 255) / 256, 4096);
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)workspace, slab, splits, cout,
+                     9 * cin, 9 * cin, dw, f);
+  return cnnitmo_check_launch("conv_wgrad_cat");
+}
+
 extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout, int n, int h,
                                       int w, int cin, int cout, float* dk, const float* fold_scale,
                                       const float* fold_shift, const float* fold_par, float* raw_out,
@@ -556,6 +586,10 @@ extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout
 // Label of the main kernel cnnitmo_conv_wgrad (ntaps 9 / 1) or
 // cnnitmo_tconv2x2_wgrad (ntaps 4) launches for these sizes (for profiles;
 // each is followed by slab_reduce_kernel).
+extern "C" const char* cnnitmo_wgrad_cat_kernel_name(int n, int h, int w, int c1, int cin, int cout) {
+  return c1 == 32 ? wgrad_halo_name(n, h, w, cin, cout, true) : "";
+}
+
 extern "C" const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, int h, int w, int cin,
                                                  int cout) {
   if (dtype == CNNITMO_BF16 && ntaps == 9) {

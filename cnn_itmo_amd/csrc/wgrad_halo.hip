@@ -48,6 +48,9 @@ struct WHArgs {
   const bf16* x;  // view [P][x_ld] at x_off
   long x_ld;
   int x_off;
+  const bf16* x2;  // CAT: input channels [32, cin) from x2 [P][x2_ld] at x2_off (x holds [0, 32))
+  long x2_ld;
+  int x2_off;
   int nimg, H, W, cin;
   float* out;  // slabs [splits][cout][9*cin]
   long slab;
@@ -57,13 +60,19 @@ struct WHArgs {
 
 // Waves: three groups (one per kernel row r = 0, 1, 2), each WM x WN over the
 // (BM, BN) block, so every wave keeps 3 taps x its tile in accumulators.
-// D: groups (dz row + x row) issued ahead; R: rows per barrier step
-template <int BM, int BN, int TW, int WM, int WN, int D, int R>
+// D: groups (dz row + x row) issued ahead; R: rows per barrier step.
+// CAT: the input is a concatenate read from its two members (model.py:261,
+// [conv1 32 | up9 64]) without a concat buffer; an x row image is then two images,
+// [XROWS][32] (KB 0..XBA) and [XROWS][BN-32] (KB XBA..), each swizzled as its own
+// width, so that every DMA instruction reads one member.
+template <int BM, int BN, int TW, int WM, int WN, int D, int R, bool CAT = false>
 struct WHCfg {
   static constexpr int NWG = WM * WN, NW = 3 * NWG, NT = NW * 64;
   static constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16, KS = TW / 32;
   static constexpr int XROWS = TW + 2;
-  static constexpr int XB = (XROWS * BN * 2 + 1023) / 1024;  // KB (= DMA instructions) per x row
+  static constexpr int XBA = CAT ? (XROWS * 32 * 2 + 1023) / 1024 : 0;  // KB of the first member's image
+  static constexpr int XB = CAT ? XBA + (XROWS * (BN - 32) * 2 + 1023) / 1024
+                                : (XROWS * BN * 2 + 1023) / 1024;  // KB (= DMA instructions) per x row
   static constexpr int DB = TW * BM * 2 / 1024;              // per dz row
   static constexpr int XS = D + R + 2, DS = D + R;           // ring slots
   static constexpr int SMEM = ((XS + 1) * XB + DS * DB) * 1024;  // + one all-zero x row
@@ -72,9 +81,10 @@ struct WHCfg {
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
-template <int BM, int BN, int TW, int WM, int WN, int D, int R>
+template <int BM, int BN, int TW, int WM, int WN, int D, int R, bool CAT = false>
 __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHArgs p) {
-  using C = WHCfg<BM, BN, TW, WM, WN, D, R>;
+  using C = WHCfg<BM, BN, TW, WM, WN, D, R, CAT>;
+  static_assert(!CAT || BN == 96, "CAT: a 32 + 64 channel input in one block");
   constexpr int NW = C::NW, TM = C::TM, TN = C::TN, FM = C::FM, FN = C::FN, KS = C::KS;
   constexpr int XB = C::XB, DB = C::DB, XS = C::XS, DS = C::DS, LX = C::LX, LD = C::LD;
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
@@ -109,11 +119,23 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
   for (int q = 0; q < LX; ++q) {
     const int ins = wave + q * NW;
     xact[q] = ins < XB;
-    const int off = ins * 1024 + lane * 16;
-    const int row = off / (BN * 2), pos = off - row * (BN * 2);
-    const int col = (((pos >> 5) ^ trswz<BN>(row)) << 4) + ((pos >> 4) & 1) * 8;
-    const int xx = x0 - 1 + row;
-    xoff[q] = row < C::XROWS && xx >= 0 && xx < p.W ? (unsigned)((row * p.x_ld + col) * 2) : dma::OOB;
+    if constexpr (CAT) {
+      const bool first = ins < C::XBA;  // an instruction of the first member's image
+      const int rw = first ? 64 : (BN - 32) * 2;
+      const int off = (first ? ins : ins - C::XBA) * 1024 + lane * 16;
+      const int row = off / rw, pos = off - row * rw;
+      const int sw = first ? trswz<32>(row) : trswz<BN - 32>(row);
+      const int col = (((pos >> 5) ^ sw) << 4) + ((pos >> 4) & 1) * 8;
+      const int xx = x0 - 1 + row;
+      const long ld = first ? p.x_ld : p.x2_ld;
+      xoff[q] = row < C::XROWS && xx >= 0 && xx < p.W ? (unsigned)((row * ld + col) * 2) : dma::OOB;
+    } else {
+      const int off = ins * 1024 + lane * 16;
+      const int row = off / (BN * 2), pos = off - row * (BN * 2);
+      const int col = (((pos >> 5) ^ trswz<BN>(row)) << 4) + ((pos >> 4) & 1) * 8;
+      const int xx = x0 - 1 + row;
+      xoff[q] = row < C::XROWS && xx >= 0 && xx < p.W ? (unsigned)((row * p.x_ld + col) * 2) : dma::OOB;
+    }
   }
   unsigned doff[LD];
   bool dact[LD];  // (the last strip may overhang the image: zero columns)
@@ -137,9 +159,15 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
     const bool ok = g >= 0 && g < total_rows;
     const long e0 = ((long)g * p.W + x0 - 1) * p.x_ld + p.x_off + n0;  // may be < 0 (first pixel)
     const i32x4 rs = dma::rsrc((uintptr_t)p.x + (uintptr_t)(e0 * 2));
+    i32x4 rs2 = rs;
+    if constexpr (CAT) {
+      const long e2 = ((long)g * p.W + x0 - 1) * p.x2_ld + p.x2_off;
+      rs2 = dma::rsrc((uintptr_t)p.x2 + (uintptr_t)(e2 * 2));
+    }
 #pragma unroll
     for (int q = 0; q < LX; ++q)
-      if (xact[q]) dma::lds16(ok ? xoff[q] : dma::OOB, rs, S + (wave + q * NW) * 1024);
+      if (xact[q]) dma::lds16(ok ? xoff[q] : dma::OOB, CAT && wave + q * NW >= C::XBA ? rs2 : rs,
+                              S + (wave + q * NW) * 1024);
   };
   auto issue_d = [&](long g, int slot) {
     char* S = dbase + slot * DB * 1024;
@@ -215,8 +243,17 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int col = wn * TN + j * 16 + 4 * pp;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s, col)));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + bfo<BN>(r0 + s + 4, col)));
+          int a0, a1;
+          if constexpr (CAT) {  // the fragment's 16 channels lie in one member's image (wave-uniform)
+            const bool first = wn * TN + j * 16 < 32;
+            a0 = first ? bfo<32>(r0 + s, col) : C::XBA * 1024 + bfo<BN - 32>(r0 + s, col - 32);
+            a1 = first ? bfo<32>(r0 + s + 4, col) : C::XBA * 1024 + bfo<BN - 32>(r0 + s + 4, col - 32);
+          } else {
+            a0 = bfo<BN>(r0 + s, col);
+            a1 = bfo<BN>(r0 + s + 4, col);
+          }
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + a0));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Xs + a1));
           bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
 #pragma unroll
@@ -286,7 +323,7 @@ struct WHPlan {
   long rows_per;
 };
 
-bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
+bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = false) {
   static const int mode = [] {
     const char* e = getenv("CNNITMO_WGRAD_HALO");
     return e ? atoi(e) : 1;
@@ -317,7 +354,10 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
       ncu = prop.multiProcessorCount;
     if (ncu <= 0) ncu = 256;
   }
-  const int xb = ((pl.tw + 2) * pl.bn * 2 + 1023) / 1024, db = pl.tw * pl.bm * 2 / 1024;
+  if (cat && !(pl.bn == 96 && cin == 96 && pl.tw == 64)) return false;  // CAT: the [32 | 64] block only
+  const int xb = cat ? ((pl.tw + 2) * 64 + 1023) / 1024 + ((pl.tw + 2) * (pl.bn - 32) * 2 + 1023) / 1024
+                     : ((pl.tw + 2) * pl.bn * 2 + 1023) / 1024,
+            db = pl.tw * pl.bm * 2 / 1024;
   const int R = wh_rows(pl.bm, pl.bn), D = R == 2 ? 3 : 2;
   const int smem = ((D + R + 3) * xb + (D + R) * db) * 1024;  // WHCfg::SMEM
   const int occ = std::max(1, (160 * 1024) / smem);
@@ -336,37 +376,47 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl) {
   return true;
 }
 
-template <int BM, int BN, int TW>
+template <int BM, int BN, int TW, bool CAT = false>
 void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
   // 12 waves (3 per SIMD) for the big blocks, 6 for the small ones
   constexpr int WM = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1), WN = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2);
   constexpr int R = wh_rows(BM, BN), D = R == 2 ? 3 : 2;
-  hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R>), dim3(grid), dim3(3 * WM * WN * 64), 0, s, a);
+  hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R, CAT>), dim3(grid), dim3(3 * WM * WN * 64), 0, s,
+                     a);
 }
 
 }  // namespace
 
-size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout) {
+size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout, bool cat) {
   WHPlan pl;
-  if (!wh_plan(n, h, w, cin, cout, pl)) return 0;
+  if (!wh_plan(n, h, w, cin, cout, pl, cat)) return 0;
   return (size_t)pl.strips * pl.rsplits * cout * 9 * cin * 4;
 }
 
 // Returns the number of slabs written (>0) or -1 when this path does not apply.
+// x2 != null: the input channels [32, cin) come from x2 (CAT; see WHCfg).
 int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n, int h, int w, int cin,
-                      int cout, float* ws, size_t ws_bytes, hipStream_t s) {
+                      int cout, float* ws, size_t ws_bytes, hipStream_t s, const bf16* x2, long x2_ld,
+                      int x2_off) {
   WHPlan pl;
-  if (!wh_plan(n, h, w, cin, cout, pl)) return -1;
-  if (x_ld % 8 || x_off % 8) return -1;
+  const bool cat = x2 != nullptr;
+  if (!wh_plan(n, h, w, cin, cout, pl, cat)) return -1;
+  if (x_ld % 8 || x_off % 8 || (cat && (x2_ld % 8 || x2_off % 8))) return -1;
   const size_t need = (size_t)pl.strips * pl.rsplits * cout * 9 * cin * 4;
   if (!ws || ws_bytes < need) return -1;
   WHArgs a;
   memset(&a, 0, sizeof(a));
   a.dz = dz; a.cout = cout; a.x = x; a.x_ld = x_ld; a.x_off = x_off;
+  a.x2 = x2; a.x2_ld = x2_ld; a.x2_off = x2_off;
   a.nimg = n; a.H = h; a.W = w; a.cin = cin;
   a.out = ws; a.slab = (long)cout * 9 * cin;
   a.strips = pl.strips; a.cbm = pl.cbm; a.cbn = pl.cbn; a.rsplits = pl.rsplits; a.rows_per = pl.rows_per;
   const unsigned grid = (unsigned)(pl.strips * pl.cbm * pl.cbn * pl.rsplits);
+  if (cat) {
+    if (pl.bm == 64) wh_launch<64, 96, 64, true>(a, grid, s);
+    else wh_launch<32, 96, 64, true>(a, grid, s);
+    return pl.strips * pl.rsplits;
+  }
 #define WH(BMv, BNv, TWv) \
   if (pl.bm == BMv && pl.bn == BNv && pl.tw == TWv) { wh_launch<BMv, BNv, TWv>(a, grid, s); return pl.strips * pl.rsplits; }
   WH(64, 96, 64) WH(64, 64, 64) WH(64, 32, 64) WH(32, 96, 64) WH(32, 64, 64) WH(32, 32, 64)
@@ -376,10 +426,10 @@ int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n
 }
 
 // kernel label for profiles ("" when this path does not apply)
-const char* wgrad_halo_name(int n, int h, int w, int cin, int cout) {
+const char* wgrad_halo_name(int n, int h, int w, int cin, int cout, bool cat) {
   WHPlan pl;
-  if (!wh_plan(n, h, w, cin, cout, pl)) return "";
+  if (!wh_plan(n, h, w, cin, cout, pl, cat)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "wgrad_halo_kernel<%d,%d,%d>", pl.bm, pl.bn, pl.tw);
+  snprintf(buf, sizeof(buf), "wgrad_halo_kernel<%d,%d,%d%s>", pl.bm, pl.bn, pl.tw, cat ? ",cat" : "");
   return buf;
 }

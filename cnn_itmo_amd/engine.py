@@ -67,12 +67,19 @@ class Value:
         self.grad_g3 = None  # (g3 [p][3], head weights [3][c]): the gradient as the head's rank-3 factor
         self.cs = None  # coefficient buffers of the owner (persist across steps)
         self.ch = None
+        self.split = False  # concat whose members keep dense buffers of their own (Engine._plan_split_concats)
 
     def owner(self):
         return self.place[0] if self.place else self
 
+    def _own_buffer(self):
+        """A member of a split concat holds its activation in a buffer of its own."""
+        return not self.place or self.place[0].split
+
     def view(self, n):
-        if self.place:
+        if self.split:
+            raise RuntimeError(f"{self.name}: a split concatenate has no single view (read its members)")
+        if not self._own_buffer():
             cv, off = self.place
             return ops.View(cv.buf, n, self.h, self.w, self.c, cv.c, off)
         return ops.View(self.buf, n, self.h, self.w, self.c, self.c, 0)
@@ -84,7 +91,9 @@ class Value:
         return ops.View(self.gbuf, n, self.h, self.w, self.c, self.c, 0)
 
     def ensure(self, n, dtype, device):
-        o = self.owner()
+        if self.split:
+            return  # the members allocate their own
+        o = self if self._own_buffer() else self.owner()
         if o.buf is None:
             o.buf = torch.empty(n * o.h * o.w * o.c, dtype=dtype, device=device)
 
@@ -196,14 +205,22 @@ class BlockStage(Stage):
             if self.kind == "c3":
                 ops.fold_conv3x3(e.dt, w32, bias, cs, ch, self.cout, self.cin, self.w_fold, self.b_fold,
                                  self.border)
-                ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fold, self.b_fold, out_view, flags, aff,
-                                stats, border=self.border)
+                if self.vin.split:
+                    a, b = self.vin.members
+                    ops.conv3x3_fwd_cat(e.dt, a.view(n), b.view(n), self.w_fold, self.b_fold, out_view, flags, aff,
+                                        stats, border=self.border)
+                else:
+                    ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fold, self.b_fold, out_view, flags, aff,
+                                    stats, border=self.border)
             else:
                 ops.fold_tconv(e.dt, w32, bias, cs, ch, self.cout, self.cin, self.w_fold, self.b_fold)
                 ops.tconv_fwd(e.dt, self.vin.view(n), self.w_fold, self.b_fold, out_view,
                               flags | L.BIAS_PER_COL, aff, stats)
             return
-        if self.kind == "c3":
+        if self.kind == "c3" and self.vin.split:
+            a, b = self.vin.members
+            ops.conv3x3_fwd_cat(e.dt, a.view(n), b.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
+        elif self.kind == "c3":
             ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
         elif self.kind == "c3in" and self.direct:
             ops.conv_c3_fwd(e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.w_fwd, bias, out_view, flags,
@@ -412,9 +429,12 @@ class BlockStage(Stage):
             ops.colsum(part2, rows, 4 * cout, 1, psum)
         else:
             ops.colsum(part2, rows, cout, 1, db)
-        # The weight gradient is off the critical path (dz -> dgrad -> next BN backward):
-        # it runs on the engine's side stream, overlapping the HBM-bound BN passes and the
-        # dgrad on the compute stream.  Tensors it reads are recorded on that stream.
+        # The weight gradient is off the critical path (dz -> dgrad -> next BN backward).
+        # With CNNITMO_SIDE_STREAM=1 it runs on a side stream beside the compute stream's
+        # dgrad and BN passes; off by default: every kernel here is persistent (one
+        # workgroup per CU), so the two streams only interleave whole CUs, and the bench
+        # measured 195.8 (one stream) vs 195.6 frames/s (profiles/r03c_*), while each
+        # side-stream kernel ran up to 3x slower in the step than alone.
         targets = self._sum_targets() if self.fold_active else []
         fz = self._fused_target(n, targets)
         # with a fused producer BN the dgrad needs this weight gradient's sums first
@@ -437,7 +457,11 @@ class BlockStage(Stage):
                     bsum = torch.empty(8 * cout, device=e.device, dtype=torch.float32)
                     ops.colsum(bpart, brows, 8 * cout, 1, bsum)
                     fold = self.vin.coef() + (db, bsum)
-                ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
+                if self.vin.split:
+                    a, b = self.vin.members
+                    ops.conv_wgrad_cat(e.dt, a.view(n), b.view(n), dz, cout, dw, fold=fold, raw=raw)
+                else:
+                    ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
                 for m, ci0 in targets:
                     pm = torch.empty(L.CONSUMER_ROWS * 2 * m.c, device=e.device, dtype=torch.float32)
                     ops.bn_consumer_sums(1, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, db,
@@ -774,6 +798,7 @@ class Engine:
         self.dt, self.tdtype = ops.DTYPES[dtype]
         self.device = torch.device(device)
         self.stages = compile_graph(model, fold=os.environ.get("CNNITMO_NO_FOLD", "0") != "1")
+        self._plan_split_concats()
         self.training = False
         self.h_valid = None
         self.update_moving = True
@@ -790,11 +815,42 @@ class Engine:
         self.step = 0
         self.grad_hook = None  # callable(lo, hi) after each stage's gradients are written
         self.fwd_hook = None  # callable() after the training forward (moving stats final)
-        self._side = None  # side stream for weight gradients (CNNITMO_SIDE_STREAM=0: off)
-        self._side_on = os.environ.get("CNNITMO_SIDE_STREAM", "1") != "0"
+        self._side = None  # side stream for weight gradients (CNNITMO_SIDE_STREAM=1: on)
+        self._side_on = os.environ.get("CNNITMO_SIDE_STREAM", "0") == "1"
         # consumer dgrads apply their producer's BN backward (CNNITMO_FUSE_BNB=0: separate pass)
         self.fuse_bnb = os.environ.get("CNNITMO_FUSE_BNB", "1") != "0"
         self._side_keep = []
+
+    def _plan_split_concats(self):
+        """Keep the members of a concatenate in dense buffers of their own when their
+        slices of a concat row would cover partial 128-B lines: the level-0 concat
+        [conv1 32 | up9 64] (model.py:261) puts 64 + 128 B of each 192-B row in lines
+        shared with the neighbouring pixels, so the pool, its BN-sum pass and enc1b's
+        BN-backward apply read conv1 in half lines and up9 writes them.  Its consumer
+        (dec9a, a 3x3 conv) then reads both members directly: cnnitmo_conv3x3_fwd_cat /
+        cnnitmo_conv_wgrad_cat (bf16 halo kernels; its input gradient is already split
+        per member).  CNNITMO_SPLIT_CAT=0: one concat buffer."""
+        if self.dt != L.BF16 or os.environ.get("CNNITMO_SPLIT_CAT", "1") == "0":
+            return
+        readers = {}
+        for st in self.stages:
+            for v in [getattr(st, "vin", None)]:
+                if v is not None:
+                    readers.setdefault(id(v), []).append(st)
+        for st in self.stages:
+            if not isinstance(st, ConcatStage):
+                continue
+            v = st.vout
+            rs = readers.get(id(v), [])
+            if len(v.members) != 2 or len(rs) != 1 or not isinstance(rs[0], BlockStage) or rs[0].kind != "c3":
+                continue
+            c1, c = v.members[0].c, v.c
+            esz = 2  # bf16
+            if (c1 * esz) % 128 == 0 and (c * esz) % 128 == 0:
+                continue  # member slices already cover whole lines
+            if not ops.wgrad_cat_supported(1, v.h, v.w, c1, c, rs[0].cout):
+                continue
+            v.split = True
 
     # ---- parameter access ---------------------------------------------------
     def _slice(self, flat, table, key):

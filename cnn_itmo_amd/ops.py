@@ -66,6 +66,14 @@ def conv3x3_fwd(dt, x: View, wt, bias, out: View, flags=0, aff=None, stats=None,
          stream_ptr())
 
 
+def conv3x3_fwd_cat(dt, x1: View, x2: View, wt, bias, out: View, flags=0, aff=None, stats=None, border=None):
+    """conv3x3_fwd over concatenate([x1, x2]) read from its members (cnnitmo_conv3x3_fwd_cat)."""
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_conv3x3_fwd_cat", dt, x1.ptr, x1.ld, x1.off, x1.c, x2.ptr, x2.ld, x2.off, x1.n, x1.h, x1.w,
+         x1.c + x2.c, ptr(wt), ptr(bias), out.c, out.ptr, out.ld, out.off, flags, ptr(sc), ptr(sh), ptr(stats),
+         ptr(border), stream_ptr())
+
+
 def conv1tap_fwd(dt, cols, k, m, wt, bias, out: View, flags=0, aff=None, stats=None):
     sc, sh = aff if aff is not None else (None, None)
     call("cnnitmo_conv1tap_fwd", dt, ptr(cols), k, m, ptr(wt), ptr(bias), out.c, out.ptr, out.ld,
@@ -122,6 +130,20 @@ def conv_wgrad(dt, ntaps, x: View, dz, cout, dw, dw_cols=0, fold=None, raw=None)
     call("cnnitmo_conv_wgrad", dt, ntaps, x.ptr, x.ld, x.off, ptr(dz), x.n, x.h, x.w, x.c, cout,
          ptr(dw), dw_cols, ptr(fs), ptr(fh), ptr(fdb), ptr(fb), ptr(raw), ws.data_ptr(), ws.numel(),
          stream_ptr())
+
+
+def conv_wgrad_cat(dt, x1: View, x2: View, dz, cout, dw, fold=None, raw=None):
+    """conv_wgrad (9 taps) over concatenate([x1, x2]) read from its members (cnnitmo_conv_wgrad_cat)."""
+    cin = x1.c + x2.c
+    ws = workspace(query("cnnitmo_wgrad_cat_workspace_bytes", x1.n, x1.h, x1.w, x1.c, cin, cout), dz.device)
+    fs, fh, fdb, fb = fold if fold is not None else (None,) * 4
+    call("cnnitmo_conv_wgrad_cat", dt, x1.ptr, x1.ld, x1.off, x1.c, x2.ptr, x2.ld, x2.off, ptr(dz), x1.n, x1.h,
+         x1.w, cin, cout, ptr(dw), ptr(fs), ptr(fh), ptr(fdb), ptr(fb), ptr(raw), ws.data_ptr(), ws.numel(),
+         stream_ptr())
+
+
+def wgrad_cat_supported(n, h, w, c1, cin, cout):
+    return query("cnnitmo_wgrad_cat_workspace_bytes", n, h, w, c1, cin, cout) > 0
 
 
 def conv_c3_stat_rows(n, h, w):

@@ -75,6 +75,18 @@ int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off, int n, in
                         const float* aff_shift, float* stat_part, const float* border,
                         void* stream);
 
+/* conv3x3_fwd over concatenate([x1, x2]) (model.py:261, Keras axis=3) read from its
+ * two members, without a concat buffer: input channels [0, c1) are x1's view
+ * (x1_ld, x1_off), channels [c1, cin) are x2's (x2_ld, x2_off).  bf16 only, c1 % 32 == 0,
+ * an epilogue (flags / bias / stats) required; CNNITMO_EUNSUPPORTED otherwise.  Used for
+ * the level-0 concat [conv1 32 | up9 64], whose members each occupy partial 128-B lines
+ * of a 192-B concat row. */
+int cnnitmo_conv3x3_fwd_cat(int dtype, const void* x1, int x1_ld, int x1_off, int c1, const void* x2,
+                            int x2_ld, int x2_off, int n, int h, int w, int cin, const void* wt,
+                            const float* bias, int cout, void* out, int out_ld, int out_off, int flags,
+                            const float* aff_scale, const float* aff_shift, float* stat_part,
+                            const float* border, void* stream);
+
 /* Name of the kernel conv3x3_fwd (dgrad = 0) / conv3x3_dgrad (dgrad = 1, same
  * layer cin/cout) launches for these sizes (profiling labels; no GPU needed). */
 const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int w, int cin, int cout,
@@ -136,6 +148,17 @@ int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
  * (cnnitmo_border_sums + cnnitmo_colsum); dw is then the exact gradient w.r.t. W.
  * All four NULL: plain weight gradient.  raw_out (nullable, same layout as dw):
  * the uncorrected sum dz (x) r, input of cnnitmo_bn_consumer_sums. */
+
+/* cnnitmo_conv_wgrad (ntaps 9, bf16) over concatenate([x1, x2]) read from its members
+ * (see cnnitmo_conv3x3_fwd_cat): c1 == 32, cin == 96 (dec9a, model.py:261-262).
+ * workspace: cnnitmo_wgrad_cat_workspace_bytes (0 = unsupported sizes). */
+size_t cnnitmo_wgrad_cat_workspace_bytes(int n, int h, int w, int c1, int cin, int cout);
+const char* cnnitmo_wgrad_cat_kernel_name(int n, int h, int w, int c1, int cin, int cout);
+int cnnitmo_conv_wgrad_cat(int dtype, const void* x1, int x1_ld, int x1_off, int c1, const void* x2, int x2_ld,
+                           int x2_off, const void* dz, int n, int h, int w, int cin, int cout, float* dw,
+                           const float* fold_scale, const float* fold_shift, const float* fold_db,
+                           const float* fold_border, float* raw_out, void* workspace, size_t ws_bytes,
+                           void* stream);
 
 /* First layer (Cin=3): pack x [n,h_valid,w,3] fp32 into [n,h,w,32] dtype
  * columns k=(r*3+s)*3+c (k<27, zero pad; rows >= h_valid are zero), so that

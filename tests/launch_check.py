@@ -126,7 +126,7 @@ class _Acc:
 
 
 # every launching entry point of cnn_itmo_amd.ops (all of them go through ops.call)
-LAUNCHES = ("conv3x3_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
+LAUNCHES = ("conv3x3_fwd", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
             "conv_wgrad", "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad", "conv1tap_fwd", "im2col_c3",
             "maxpool_fwd", "maxpool_bwd", "pool_bnsums", "bn_fwd_finalize", "bn_infer_coeffs", "bn_apply",
             "bn_bwd_reduce", "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3",
@@ -206,9 +206,9 @@ class LaunchChecker(ElementwiseChecks):
         assert worst <= 1.0, f"{label}: partial-sum totals off ({worst:.2f} x bound)"
 
     # ---- conv3x3 -------------------------------------------------------------------
-    def _chk_conv3x3_fwd(self, dt, x, wt, bias, out, flags=0, aff=None, stats=None, border=None):
+    def _chk_conv3x3_fwd(self, dt, x, wt, bias, out, flags=0, aff=None, stats=None, border=None, tag=""):
         n, h, w, cin, cout = x.n, x.h, x.w, x.c, out.c
-        lab = f"conv3x3_fwd {n}x{h}x{w} {cin}->{cout}"
+        lab = f"conv3x3_fwd{tag} {n}x{h}x{w} {cin}->{cout}"
         W = wt.view(cout, 3, 3, cin)
         bmap = _border_map(border, h, w, wt.device) if border is not None else 0
         acc = _Acc(self, lab)
@@ -234,6 +234,19 @@ class LaunchChecker(ElementwiseChecks):
             tot = stats.view(-1, 2, cout).to(F64).sum(0)
             self._sums(lab + " stats", tot[0], s1, sa)
             self._sums(lab + " stats^2", tot[1], s2, sa2)
+
+    @staticmethod
+    def _cat_view(x1, x2):
+        """The concatenate [x1, x2] (channels) as one dense View (a copy; test only)."""
+        t = torch.cat([x1.tensor(), x2.tensor()], dim=3).contiguous()
+        from cnn_itmo_amd.ops import View
+        return View(t.view(-1), x1.n, x1.h, x1.w, x1.c + x2.c, x1.c + x2.c, 0)
+
+    def _chk_conv3x3_fwd_cat(self, dt, x1, x2, wt, bias, out, flags=0, aff=None, stats=None, border=None):
+        self._chk_conv3x3_fwd(dt, self._cat_view(x1, x2), wt, bias, out, flags, aff, stats, border, tag="_cat")
+
+    def _chk_conv_wgrad_cat(self, dt, x1, x2, dz, cout, dw, fold=None, raw=None):
+        self._chk_conv_wgrad(dt, 9, self._cat_view(x1, x2), dz, cout, dw, fold=fold, raw=raw, tag="_cat")
 
     def _chk_conv3x3_dgrad(self, dt, dz, n, h, w, cout, wflip, cin, dx):
         d4, Wf, dxt = dz.view(n, h, w, cout), wflip.view(-1)[:cin * 9 * cout].view(cin, 3, 3, cout), dx.tensor()
@@ -286,9 +299,9 @@ class LaunchChecker(ElementwiseChecks):
         tot = part.view(-1, npar, c).to(F64).sum(0)
         self._sums(lab + " part", tot, ps, pa)
 
-    def _chk_conv_wgrad(self, dt, ntaps, x, dz, cout, dw, dw_cols=0, fold=None, raw=None):
+    def _chk_conv_wgrad(self, dt, ntaps, x, dz, cout, dw, dw_cols=0, fold=None, raw=None, tag=""):
         n, h, w, cin = x.n, x.h, x.w, x.c
-        lab = f"conv_wgrad({ntaps}) {n}x{h}x{w} {cin}->{cout}"
+        lab = f"conv_wgrad{tag}({ntaps}) {n}x{h}x{w} {cin}->{cout}"
         xt, d4 = x.tensor(), dz.view(n, h, w, cout)
         if ntaps == 1:  # im2col columns (fp32 first layer): dw [cout][dw_cols or cin]
             kc = dw_cols or cin

@@ -71,7 +71,7 @@ def _run(h, w, batch, dtype, train, expect):
     assert not missing, f"entry points never launched/checked: {missing}"
 
 
-TRAIN = ["conv_c3_fwd", "conv3x3_fwd", "tconv_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_dgrad",
+TRAIN = ["conv_c3_fwd", "conv3x3_fwd", "conv3x3_fwd_cat", "conv_wgrad_cat", "tconv_fwd", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_dgrad",
          "tconv_dgrad_bn", "conv_wgrad", "tconv_wgrad", "conv_c3_wgrad",
          "maxpool_fwd", "maxpool_bwd", "pool_bnsums", "bn_fwd_finalize", "bn_apply", "bn_bwd_reduce",
          "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3", "bn_consumer_sums", "colsum",
@@ -103,6 +103,6 @@ def test_config4_train_4k_b8_bf16():
 def test_small_frame_all_launch_kinds(dtype):
     """The same per-launch checks on a small ragged frame (quick; every kind)."""
     # fp32 training runs the unfused BN backward (no *_dgrad_bn) and the im2col first layer
-    exp = TRAIN if dtype == "bfloat16" else [k for k in TRAIN if not k.startswith("conv_c3") and "dgrad_bn" not in k] \
-        + ["im2col_c3", "conv1tap_fwd"]
+    exp = TRAIN if dtype == "bfloat16" else [k for k in TRAIN if not k.startswith("conv_c3") and "dgrad_bn" not in k
+                                             and "_cat" not in k] + ["im2col_c3", "conv1tap_fwd"]
     _run(72, 112, 2, dtype, True, exp)

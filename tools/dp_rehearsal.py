@@ -10,9 +10,13 @@ Checks (rank 0):
   * they equal a single-process replay that draws the UNSHARDED stream at the
     global batch size (batch * world), splits each global batch into the ranks'
     shares, runs each share with that rank's dropout seed from the same starting
-    state, weights each share's batch-mean gradient by its share of the global batch
-    (the 11-frame stream ends in a 3-frame global batch: shares 2 and 1), averages
-    the moving statistics itself and applies RMSprop once;
+    state, weights each share's gradient by its share of the global batch (the
+    11-frame stream ends in a 3-frame global batch: shares 2 and 1), averages the
+    moving statistics itself and applies RMSprop once.  fp32: the replay weights the
+    shares' batch-mean gradients by n_r/N itself (the semantics, independently); bf16:
+    it normalises each share's loss gradient by N/world frames as the DP path does (the
+    same roundings: near-zero gradients would otherwise flip sign, and RMSprop's first
+    step moves every such weight by a full +-lr*sqrt(10));
   * the epoch loss equals the sample-weighted mean of the replay's per-share losses.
 
   CNNITMO_DEVICE=0 CNNITMO_DIST_BACKEND=gloo python -m torch.distributed.run \\
@@ -88,14 +92,18 @@ def main():
             for k, ix in enumerate(parts):
                 e2.bufs.copy_(b0)
                 ix = torch.as_tensor(ix, device=xb.device)
-                la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False)
+                if dtype == "float32":
+                    la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False)
+                    acc += e2.grads * (len(ix) / len(xb))  # the global batch mean's gradient
+                else:
+                    la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False, grad_frames=len(xb) / world)
+                    acc += e2.grads
                 lsum += float(la[0]) * len(ix)
                 nsum += len(ix)
-                acc += e2.grads * (len(ix) / len(xb))  # the global batch mean's gradient
                 bacc += e2.bufs
             e2.step -= world - 1
             e2.bufs.copy_(bacc * (1.0 / world))
-            ops.rmsprop(e2.params, acc, e2.accum, 1e-3, 0.9, 1e-7, 1.0)
+            ops.rmsprop(e2.params, acc, e2.accum, 1e-3, 0.9, 1e-7, 1.0 if dtype == "float32" else 1.0 / world)
             e2.weights_dirty = True
         torch.cuda.synchronize()
         q = e2.params.cpu().numpy()
