@@ -21,6 +21,30 @@ __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ in,
   }
 }
 
+// copy with cache-policy variants (MODE 0: nt load + nt store, 1: nt store, 2: nt load,
+// 3: plain load + sc1 store (write-through, the line is dropped from L2))
+template <int U, int MODE>
+__global__ __launch_bounds__(256) void copyp_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out, long n) {
+  const long step = (long)gridDim.x * 256 * U;
+  for (long b = (long)blockIdx.x * 256 * U + threadIdx.x; b < n; b += step) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = b + u * 256;
+      if (MODE == 0 || MODE == 2) v[u] = i < n ? __builtin_nontemporal_load(in + i) : u32x4{0, 0, 0, 0};
+      else v[u] = i < n ? in[i] : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = b + u * 256;
+      if (i >= n) continue;
+      if (MODE == 0 || MODE == 1) __builtin_nontemporal_store(v[u], out + i);
+      else if (MODE == 3) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(out + i), "v"(v[u]) : "memory");
+      else out[i] = v[u];
+    }
+  }
+}
+
 // sum of everything (pure read)
 template <int U>
 __global__ __launch_bounds__(256) void read_kernel(const u32x4* __restrict__ in, long n, unsigned* sink) {
@@ -102,11 +126,18 @@ extern "C" int hbm_probe(int kind, int u, int pf, const void* a, const void* b, 
 #define ARGS A, O, nvec
     DISP(copy_kernel)
 #undef ARGS
+  } else if (kind >= 16 && kind < 20) {
+#define ARGS A, O, nvec
+    if (kind == 16) { DISP(copyp_kernel, , 0) }
+    else if (kind == 17) { DISP(copyp_kernel, , 1) }
+    else if (kind == 18) { DISP(copyp_kernel, , 2) }
+    else { DISP(copyp_kernel, , 3) }
+#undef ARGS
   } else if (kind == 1) {
 #define ARGS A, nvec, (unsigned*)O
     DISP(read_kernel)
 #undef ARGS
-  } else if (kind >= 4) {  // part_kernel, ps = kind
+  } else if (kind >= 4 && kind < 16) {  // part_kernel, ps = kind
 #define ARGS A, nvec, kind, (unsigned*)O
     DISP(part_kernel)
 #undef ARGS

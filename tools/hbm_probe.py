@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--gb", type=float, default=8.5)
     ap.add_argument("--part", action="store_true", help="partial-line reads (FETCH_SIZE calibration)")
+    ap.add_argument("--copy-policies", action="store_true",
+                    help="copy with nt / sc1 cache policies (the guide's 6.29 TB/s float4 copy vs this box's plain copy)")
     a = ap.parse_args()
     if a.build:
         return build()
@@ -51,11 +53,18 @@ def main():
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
         t = sorted(ts)[2]
-        nbytes = nv * 16 * (2 if kind == 0 else 3 if kind == 2 else 1)
-        name = ['copy', 'read', 'apply'][kind] if kind < 4 else f"part{kind * 16}"
+        nbytes = nv * 16 * (2 if kind == 0 or kind >= 16 else 3 if kind == 2 else 1)
+        name = ['copy', 'read', 'apply'][kind] if kind < 4 else (
+            ["copy ntld+ntst", "copy ntst", "copy ntld", "copy sc1st"][kind - 16] if kind >= 16 else f"part{kind * 16}")
         print(f"{name:8s} U={u} pf={pf} grid={grid:5d}  {t:7.3f} ms  {nbytes / t / 1e9:5.2f} TB/s useful "
               f"({nbytes / 1e9:.2f} GB)", flush=True)
 
+    if a.copy_policies:
+        for kind in (0, 16, 17, 18, 19):
+            for u in (1, 4, 8):
+                for grid in (512, 1024, 2048):
+                    run(kind, u, 0, grid)
+        return
     if a.part:  # useful 64 B per pixel of ps*16 bytes; nvec/3 useful vectors (fits the 8.5 GB buffer at ps 12)
         for ps in (4, 8, 12):
             run(ps, 8, 0, 2048, nuse=nvec // 3)
