@@ -66,7 +66,7 @@ struct TSArgs {
   int flags;
   const float* aff_scale;
   const float* aff_shift;
-  float* stats;  // MODE 0: [ntiles*WM][2][N]; MODE 1 EPI: [ntiles*WM][N] sums of dz
+  float* stats;  // MODE 0: [G*WM][2][N]; MODE 1 EPI: [G*WM][N] sums of dz (G = gridDim / nblocks)
   const float* coef;  // MODE 1 EPI: [3][N]
   const bf16* r;
   long r_ld;
@@ -112,7 +112,15 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   const int nb = lid % p.nblocks, g = lid / p.nblocks;
   const long per = (p.ntiles + G - 1) / G;
   const long t0 = (long)g * per, t1 = t0 + per < p.ntiles ? t0 + per : p.ntiles;
-  if (t0 >= t1) return;
+  if (t0 >= t1) {  // no tiles: this group's partial-sum rows are zero
+    const bool st = MODE == 0 ? (p.flags & CNNITMO_STATS) != 0 : EPI;
+    const int wm = wave / C::WN;
+    const long row = (long)g * C::WM + wm;
+    const int cols = (MODE == 0 ? 2 : 1) * p.N;
+    if (st && lid % p.nblocks == 0)  // one workgroup per group: the rows span all N columns
+      for (int i = (wave % C::WN) * 64 + lane; i < cols; i += C::WN * 64) p.stats[(size_t)row * cols + i] = 0.f;
+    return;
+  }
   const int K = p.K, nch = K / C::KC, n0 = nb * BN;
 
   // ---- resident weight block + per-column parameters (once) -------------------
@@ -240,16 +248,19 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   constexpr int FP = FN / 2;
   static_assert(FN % 2 == 0, "column pairs");
   constexpr int SOUT = FM * FP;
-  const int S = SOUT + (MODE == 0 ? (stats ? 4 * FP : 0) : (EPI ? 2 * FP : 0));
+  const int S = SOUT;
   typedef float f32x8_ __attribute__((ext_vector_type(8)));
+  // BN partial sums of the lane's pixels, kept in registers for the whole launch (the
+  // workgroup's columns never change): one row per (workgroup group, wave row) at the
+  // end instead of one per tile (up9: 1 GB of fp32 partials per step before)
+  float s1[FP][8], s2[FP][8];
+#pragma unroll
+  for (int j = 0; j < FP; ++j)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s1[j][k] = s2[j][k] = 0.f;
   auto epilogue = [&](long t, int rslot) {
     int img, y, x0;
     tile_pos(t, img, y, x0);
-    float s1[FP][8], s2[FP][8];
-#pragma unroll
-    for (int j = 0; j < FP; ++j)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s1[j][k] = s2[j][k] = 0.f;
     if constexpr (MODE == 0) {
       const __amdgpu_buffer_rsrc_t os =
           srsrc(p.out + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.out_ld + p.out_off);
@@ -277,29 +288,6 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
           }
           const unsigned off = (unsigned)((((tap >> 1) * W2 + 2 * px + (tap & 1)) * p.out_ld + co) * 2);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, o), os, ok ? off : OOB, 0, 0);
-        }
-      }
-      if (stats) {
-        const long row = (t * C::WM + wm);
-        const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)row * 2 * p.N);
-#pragma unroll
-        for (int jp = 0; jp < FP; ++jp) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            s1[jp][k] = row16_sum(s1[jp][k]);
-            s2[jp][k] = row16_sum(s2[jp][k]);
-          }
-          const int n = n0 + wn * (BN / WN) + jp * 32 + (lane >> 4) * 8;
-          const bool w0 = (lane & 15) == 0;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f32x4_ a1 = {s1[jp][4 * h], s1[jp][4 * h + 1], s1[jp][4 * h + 2], s1[jp][4 * h + 3]};
-            const f32x4_ a2 = {s2[jp][4 * h], s2[jp][4 * h + 1], s2[jp][4 * h + 2], s2[jp][4 * h + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss,
-                                                   w0 ? (unsigned)((n + 4 * h) * 4) : OOB, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a2), ss,
-                                                   w0 ? (unsigned)((p.N + n + 4 * h) * 4) : OOB, 0, 0);
-          }
         }
       }
     } else {
@@ -336,21 +324,6 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
                                                  ok ? (unsigned)((px * p.out_ld + n0 + c) * 2) : OOB, 0, 0);
         }
       }
-      if constexpr (EPI) {
-        const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)(t * C::WM + wm) * p.N);
-#pragma unroll
-        for (int jp = 0; jp < FP; ++jp) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) s1[jp][k] = row16_sum(s1[jp][k]);
-          const int n = n0 + wn * (BN / WN) + jp * 32 + (lane >> 4) * 8;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f32x4_ a1 = {s1[jp][4 * h], s1[jp][4 * h + 1], s1[jp][4 * h + 2], s1[jp][4 * h + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss,
-                                                   (lane & 15) == 0 ? (unsigned)((n + 4 * h) * 4) : OOB, 0, 0);
-          }
-        }
-      }
     }
     zero();
   };
@@ -385,6 +358,32 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
 #pragma unroll
     for (int k = 0; k < ST - 1; ++k) mq[k] = mq[k + 1];
     slot = slot == ST - 1 ? 0 : slot + 1;
+  }
+  // the launch's partial sums: row (g, wm), the 16 pixel lanes of each fragment folded
+  if ((MODE == 0 && stats) || (MODE == 1 && EPI)) {
+    const long row = (long)g * C::WM + wm;
+    const __amdgpu_buffer_rsrc_t ss = srsrc(p.stats + (size_t)row * (MODE == 0 ? 2 : 1) * p.N);
+#pragma unroll
+    for (int jp = 0; jp < FP; ++jp) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        s1[jp][k] = row16_sum(s1[jp][k]);
+        if (MODE == 0) s2[jp][k] = row16_sum(s2[jp][k]);
+      }
+      const int n = n0 + wn * (BN / WN) + jp * 32 + (lane >> 4) * 8;
+      const bool w0 = (lane & 15) == 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4_ a1 = {s1[jp][4 * h], s1[jp][4 * h + 1], s1[jp][4 * h + 2], s1[jp][4 * h + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a1), ss, w0 ? (unsigned)((n + 4 * h) * 4) : OOB,
+                                               0, 0);
+        if (MODE == 0) {
+          const f32x4_ a2 = {s2[jp][4 * h], s2[jp][4 * h + 1], s2[jp][4 * h + 2], s2[jp][4 * h + 3]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, a2), ss,
+                                                 w0 ? (unsigned)((p.N + n + 4 * h) * 4) : OOB, 0, 0);
+        }
+      }
+    }
   }
 }
 
@@ -449,11 +448,15 @@ bool tconv_stream_handles(int mode, int h, int w, int cin, int cout, bool epi) {
   return ts_plan(mode, h, w, cin, cout, epi, pl);
 }
 
+// launch grid: 8 | grid and nblocks | grid / 8 (XCD-aware mapping in the kernel)
+int ts_grid(int nblocks) { return 8 * std::max(nblocks, num_cus() / 8 / nblocks * nblocks); }
+
 long tconv_stream_rows(int mode, int n, int h, int w, int cin, int cout, bool epi) {
   TSPlan pl;
   if (!ts_plan(mode, h, w, cin, cout, epi, pl)) return 0;
-  const int wm = pl.bn >= 128 ? 2 : 8 / (pl.bn / 32);  // TSCfg::WM: one row per pixel wave-row
-  return (long)n * h * ((w + 63) / 64) * wm;
+  const int wm = pl.bn >= 128 ? 2 : 8 / (pl.bn / 32);  // TSCfg::WM: one row per (workgroup group, wave row)
+  const int nblocks = (mode == 0 ? 4 * cout : cin) / pl.bn;
+  return (long)ts_grid(nblocks) / nblocks * wm;
 }
 
 const char* tconv_stream_name(int mode, int h, int w, int cin, int cout, bool epi) {
@@ -487,9 +490,7 @@ int launch_tconv_stream(int mode, const void* a, long a_ld, int a_off, const voi
   t.coef = coef; t.r = (const bf16*)r; t.r_ld = r_ld; t.r_off = r_off;
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || stats, "%s: STATS without buffer", what);
   CNN_REQUIRE(!epi || stats, "%s: fused BN backward without a sums buffer", what);
-  // 8 | grid and nblocks | grid / 8 (XCD-aware mapping in the kernel)
-  const int per_xcd = std::max(t.nblocks, num_cus() / 8 / t.nblocks * t.nblocks);
-  const int grid = 8 * per_xcd;
+  const int grid = ts_grid(t.nblocks);
 #define L1(M, B, S, E) ts_launch<M, B, S, E>(t, grid, s)
   if (mode == 0) {
     if (pl.bn == 256) L1(0, 256, 5, false);

@@ -308,15 +308,21 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 // results): no s_barrier -11 %, no vmcnt wait -11 %, no row DMA -15 %, none of the
 // three -24 % (1.15 -> 1.5 PF/s: the MFMA + fragment-read loop alone); prefetching 4
 // rows ahead instead of 2 changed nothing.  So the 64 x 96 block (one workgroup per CU
-// at any ring size) multiplies two rows per wait + barrier, 3 groups ahead (144 KB);
+// at any ring size) multiplies three rows per wait + barrier, 2 groups ahead (144 KB;
+// dec6-dec9 23.02 vs 23.27 ms at two rows / 3 ahead, profiles/r03g_ab_wgrad_rows.txt);
 // the smaller blocks keep one row per step (two workgroups per CU).
 #ifndef WH_ROWS96
-#define WH_ROWS96 2
+#define WH_ROWS96 3
 #endif
 #ifndef WH_ROWS_SMALL
 #define WH_ROWS_SMALL 1
 #endif
 constexpr int wh_rows(int bm, int bn) { return bm == 64 && bn == 96 ? WH_ROWS96 : WH_ROWS_SMALL; }
+// row groups issued ahead
+#ifndef WH_AHEAD96
+#define WH_AHEAD96 2
+#endif
+constexpr int wh_ahead(int r) { return r == WH_ROWS96 && WH_ROWS96 > 1 ? WH_AHEAD96 : 2; }
 
 struct WHPlan {
   int bm, bn, tw, strips, cbm, cbn, rsplits, smem;
@@ -358,7 +364,7 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
   const int xb = cat ? ((pl.tw + 2) * 64 + 1023) / 1024 + ((pl.tw + 2) * (pl.bn - 32) * 2 + 1023) / 1024
                      : ((pl.tw + 2) * pl.bn * 2 + 1023) / 1024,
             db = pl.tw * pl.bm * 2 / 1024;
-  const int R = wh_rows(pl.bm, pl.bn), D = R == 2 ? 3 : 2;
+  const int R = wh_rows(pl.bm, pl.bn), D = wh_ahead(R);
   const int smem = ((D + R + 3) * xb + (D + R) * db) * 1024;  // WHCfg::SMEM
   const int occ = std::max(1, (160 * 1024) / smem);
   const long slots = (long)ncu * occ;
@@ -380,7 +386,7 @@ template <int BM, int BN, int TW, bool CAT = false>
 void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
   // 12 waves (3 per SIMD) for the big blocks, 6 for the small ones
   constexpr int WM = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1), WN = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2);
-  constexpr int R = wh_rows(BM, BN), D = R == 2 ? 3 : 2;
+  constexpr int R = wh_rows(BM, BN), D = wh_ahead(R);
   hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R, CAT>), dim3(grid), dim3(3 * WM * WN * 64), 0, s,
                      a);
 }
