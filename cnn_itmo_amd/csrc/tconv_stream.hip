@@ -406,8 +406,9 @@ bool ts_plan(int mode, int h, int w, int cin, int cout, bool epi, TSPlan& pl) {
   if (!bn || N % bn) return false;
   if (epi && bn > 128) bn = 128;  // LDS: two r slots of 64 x BN
   // one column block only: with several, every block streams all of A again and
-  // the per-CU LDS-DMA rate (not HBM) becomes the bound (measured slower than the
-  // halo / igemm paths for up6..up8)
+  // the per-CU LDS-DMA rate (not HBM) becomes the bound: up6 / up7 / up8 forward
+  // 2.51 / 4.93 / 3.03 ms against tconv_ws's 0.83 / 1.72 / 2.40
+  // (profiles/r03i_ab_tconv_stream_multiblock.txt)
   if (N != bn) return false;
   pl.bn = bn;
   pl.epi = epi;
