@@ -23,7 +23,7 @@ LAYERS = [
     ("enc4b", "c3", 3, 256, 256), ("crossa", "c3", 4, 256, 512), ("crossb", "c3", 4, 512, 512),
     ("up6", "t2", 4, 512, 512), ("dec6", "c3", 3, 768, 512), ("up7", "t2", 3, 512, 256),
     ("dec7", "c3", 2, 384, 256), ("up8", "t2", 2, 256, 128), ("dec8", "c3", 1, 192, 128),
-    ("up9", "t2", 1, 128, 64), ("dec9", "c3", 0, 96, 64),
+    ("up9", "t2", 1, 128, 64), ("dec9", "c3", 0, 96, 64), ("dec9b", "c3", 0, 64, 64),
 ]
 
 
@@ -87,18 +87,20 @@ def main():
             if "dgrad" in want:
                 dx = ops.new_view(B, h, w, cin, T)
                 rows.append((name, "dgrad", fl, timeit(lambda: ops.conv3x3_dgrad(dt, out.buf, B, h, w, cout, wt, cin, dx), a.iters)))
-            if "dgradbn" in want and name.startswith("dec"):
+            if "dgradbn" in want and (name.startswith("dec") or lvl == 0):
                 # decoder dgrad with the up-path producer's BN backward fused (engine: concat
-                # [skip, up], up = the tconv output at channels [cin - cout, cin), parity sums)
-                c0, c1 = cin - cout, cin
+                # [skip, up], up = the tconv output at channels [cin - cout, cin), parity sums);
+                # a level-0 conv whose whole input is the previous conv's BN output: [0, cin)
+                par = name.startswith("dec") and name != "dec9b"
+                c0, c1 = (cin - cout, cin) if par else (0, cin)
                 dx = ops.new_view(B, h, w, cin, T)
-                r = ops.View(x.buf, B, h, w, cout, cin, c0)
-                coef = torch.rand(3 * cout, device="cuda")
+                r = ops.View(x.buf, B, h, w, c1 - c0, cin, c0)
+                coef = torch.rand(3 * (c1 - c0), device="cuda")
                 rows_ = ops.conv3x3_dgrad_bn_rows(dt, B, h, w, cout, cin, c0, c1)
-                dzp = torch.empty(B * h * w * cout, dtype=T, device="cuda")
-                pp = torch.empty(rows_ * 4 * cout, device="cuda")
+                dzp = torch.empty(B * h * w * (c1 - c0), dtype=T, device="cuda")
+                pp = torch.empty(rows_ * 4 * (c1 - c0), device="cuda")
                 rows.append((name, "dgradbn", fl, timeit(lambda: ops.conv3x3_dgrad_bn(
-                    dt, out.buf, B, h, w, cout, wt, cin, dx, c0, c1, coef, r, dzp, pp, True), a.iters)))
+                    dt, out.buf, B, h, w, cout, wt, cin, dx, c0, c1, coef, r, dzp, pp, par), a.iters)))
             if "wgrad" in want:
                 dw = torch.empty(cout * 9 * cin, device="cuda", dtype=torch.float32)
                 rows.append((name, "wgrad", fl, timeit(lambda: ops.conv_wgrad(dt, 9, x, out.buf, cout, dw), a.iters)))
