@@ -6,12 +6,17 @@
 // predict.py:59's pad-to-16 rows), so the layer reads 12 B and writes 64 B per
 // pixel instead of 12 + 64 (im2col) + 64 + 64 (GEMM):
 //
-//   conv_c3_fwd_kernel    one workgroup = RPB output rows x 256 pixels; the RPB+2
-//                         input rows are staged once; per row: A tile [256 px][32 k]
-//                         (k = (r*3+s)*3 + c, 27 used), 8 MFMAs 16x16x32 per wave
-//                         against the [32 cout][32 k] weights held in registers,
-//                         epilogue bias + ReLU (+ inference BN affine) + BN partial
-//                         sums (one row per workgroup), 16-byte stores of the bf16 row.
+//   conv_c3_fwd_kernel    persistent (3 workgroups per CU); unit = RPB output rows x
+//                         256 pixels, its RPB+2 input rows LDS-DMA'd double-buffered
+//                         (the next unit's in flight); the MFMA operand is built from
+//                         the fp32 LDS image in registers (lane = pixel), 8 MFMAs
+//                         16x16x32 per wave and row against the weights held in
+//                         registers, epilogue bias + ReLU (+ inference BN affine) +
+//                         BN partial sums (one row per workgroup for the launch),
+//                         one 16-byte store per (pixel, 8 channels) from registers.
+//                         1.82 -> 1.07 ms at 1088x1920 b32 (4.7 TB/s; the earlier
+//                         one-shot design staged the rows with scalar loads and
+//                         built A and C tiles in LDS behind four barriers per row).
 //   conv_c3_wgrad_kernel  dW[co][k] = sum_p dz[p][co] * col[p][k]: per 256-pixel unit
 //                         the dz row and the columns go to LDS as [pixel][32] rows
 //                         and are read transposed (ds_read_b64_tr_b16: pixels are
@@ -20,17 +25,36 @@
 //                         slab per workgroup, fixed-order fold.
 //
 // HBM-bound: fwd 12 B read + 64 B written per pixel (+ stats), wgrad 12 + 64 B read.
+#include "dma.h"
 #include "igemm_common.h"
 
 namespace {
 
 constexpr int SEG = 256;  // pixels per row segment (one per thread)
 constexpr int RPB = 4;    // output rows per forward workgroup
-constexpr int ALD = 40;   // A/C tile row stride in bf16 (80 B)
 
-struct C3Fwd {
+// Persistent forward: workgroup b takes units b, b + G, ... (unit = RPB output rows x
+// 256 pixels).  The unit's RPB+2 input rows (264 pixels from w0-4, so every 16-byte
+// piece is aligned to the row's 4-pixel grid) go to LDS by LDS-DMA, double-buffered:
+// the next unit's pieces are in flight while the current unit is computed.  Each wave
+// owns 64 pixels of a row and builds its MFMA operand straight from the fp32 image
+// (lane = pixel, 8 k-values per lane group); the MFMA runs with the operands swapped
+// and pair_perm weight rows, so a lane holds 8 consecutive output channels of one
+// pixel: one 16-byte store per (pixel, 8 channels) from registers, no barrier in the
+// row loop.
+constexpr int XPW = SEG + 8;                // staged pixels per row (w0-4 .. w0+SEG+4)
+constexpr int XRW = XPW * 3;                // floats per staged row (792)
+constexpr int XPC = XRW / 4;                // 16-byte pieces per staged row (198)
+constexpr int XNI = ((RPB + 2) * XPC + 63) / 64;  // 64-piece DMA instructions per unit (19)
+constexpr int XBUF = XNI * 64 * 4;          // floats per LDS buffer (sink-padded)
+#ifndef C3_GRID
+#define C3_GRID 768                         // persistent workgroups (3 per CU on 256 CUs)
+#endif
+
+struct C3Fwd2 {
   const float* x;
   int n, hv, h, w, segs, rpn;
+  long units;
   const bf16* wt;  // [32 cout][32 k]
   const float* bias;
   bf16* out;
@@ -39,109 +63,145 @@ struct C3Fwd {
   int flags;
   const float* aff_scale;
   const float* aff_shift;
-  float* stats;  // [blocks][2][32]
+  float* stats;  // [gridDim.x][2][32]
 };
 
-__device__ __forceinline__ void stage_rows(const float* __restrict__ x, int n, int hv, int w, int hfirst, int nrows,
-                                           int w0, float* xs) {
-  constexpr int PWC = (SEG + 2) * 3;
-  for (int i = threadIdx.x; i < nrows * PWC; i += 256) {
-    const int r = i / PWC, q = i - r * PWC;
-    const int hh = hfirst + r, ww = w0 - 1 + q / 3;
-    float v = 0.f;
-    if (hh >= 0 && hh < hv && ww >= 0 && ww < w) v = x[(((long)n * hv + hh) * w + ww) * 3 + q % 3];
-    xs[r * PWC + q] = v;
-  }
-}
-
-// the 32 column values (27 taps x channels + 5 zeros) of pixel t, input rows xs[r0 .. r0+2]
-__device__ __forceinline__ void patch(const float* xs, int r0, int t, float* v) {
-  constexpr int PWC = (SEG + 2) * 3;
-#pragma unroll
-  for (int k = 0; k < 32; ++k) {
-    const int tap = k / 3, c = k - tap * 3;
-    v[k] = k < 27 ? xs[(r0 + tap / 3) * PWC + (t + tap % 3) * 3 + c] : 0.f;
-  }
-}
-
-__global__ __launch_bounds__(256) void conv_c3_fwd_kernel(const C3Fwd a) {
-  __shared__ float xs[(RPB + 2) * (SEG + 2) * 3];
-  __shared__ __attribute__((aligned(16))) bf16 at[SEG * ALD];
+#ifndef C3_MINW
+#define C3_MINW 3                           // waves per SIMD the register budget is sized for
+#endif
+template <bool AFF>
+__global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 a) {
+  __shared__ __attribute__((aligned(1024))) float xs[2][XBUF];
   __shared__ float red[4][2][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int seg = blockIdx.x % a.segs;
-  const long rb = blockIdx.x / a.segs;
-  const int n = (int)(rb / a.rpn), h0 = (int)(rb % a.rpn) * RPB;
-  const int w0 = seg * SEG, npx = min(SEG, a.w - w0);
-  const int nrow = min(RPB, a.h - h0);
-  stage_rows(a.x, n, a.hv, a.w, h0 - 1, nrow + 2, w0, xs);
-  const int frow = lane & 15, fk = lane >> 4;
+  const int g = lane >> 4, pxl = lane & 15;
+  const long G = gridDim.x;
+  const int w3 = a.w * 3;
+  // K order of this kernel (k' = 8g + e): lane groups 0-2 take kernel row r = g, its 9
+  // consecutive (s, c) floats 0..7; group 3 takes float 8 of rows 0-2 and five zeros.
+  // So a lane reads its 8 values at base + e * stride (stride 1 or one staged row).
+  // (group 3's five zero slots re-read its first value: finite input times a zero weight)
+  const int kb = (g < 3 ? g : 0) * XRW + (g < 3 ? 0 : 8);
+  int koff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) koff[e] = g < 3 ? e : (e < 3 ? e * XRW : 0);
+  // weights (A operand: row i of block j = output channel pair_perm(16j + i), its
+  // k' values gathered from the [32 cout][32 k] (k = tap*3 + c) rows)
   uint4 bw[2];
-  float bj[2], sj[2], hj[2];
-  const bool relu = a.flags & CNNITMO_RELU, aff = a.flags & CNNITMO_AFFINE, stats = a.flags & CNNITMO_STATS;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int co = j * 16 + frow;
-    bw[j] = *reinterpret_cast<const uint4*>(a.wt + co * 32 + fk * 8);
-    bj[j] = a.bias ? a.bias[co] : 0.f;
-    sj[j] = aff ? a.aff_scale[co] : 1.f;
-    hj[j] = aff ? a.aff_shift[co] : 0.f;
+    const bf16* wr = a.wt + pair_perm(16 * j + pxl) * 32;
+    bf16x8 t;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = g < 3 ? wr[9 * g + e] : (e < 3 ? wr[9 * e + 8] : (bf16)0.f);
+    bw[j] = __builtin_bit_cast(uint4, t);
   }
-  float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
-  __syncthreads();
-  for (int rr = 0; rr < nrow; ++rr) {
-    {
-      float v[32];
-      patch(xs, rr, tid, v);
+  const bool relu = a.flags & CNNITMO_RELU, stats = a.flags & CNNITMO_STATS;
+  float bj[8], sj[AFF ? 8 : 1], hj[AFF ? 8 : 1], s1[8], s2[8];
 #pragma unroll
-      for (int j = 0; j < 32; j += 8) Pack16<bf16>::store(at + tid * ALD + j, v + j);
+  for (int k = 0; k < 8; ++k) {
+    const int co = 8 * g + k;
+    bj[k] = a.bias ? a.bias[co] : 0.f;
+    if constexpr (AFF) {
+      sj[k] = a.aff_scale[co];
+      hj[k] = a.aff_shift[co];
     }
-    __syncthreads();
-    f32x4 acc[4][2];
+    s1[k] = s2[k] = 0.f;
+  }
+  struct Unit {
+    int img, h0, w0;
+  };
+  auto unit = [&](long u) {
+    const int seg = (int)(u % a.segs);
+    const long rb = u / a.segs;
+    return Unit{(int)(rb / a.rpn), (int)(rb % a.rpn) * RPB, seg * SEG};
+  };
+  // the unit's pieces: instruction t (pieces 64t .. 64t+63) by wave t % 4
+  auto issue = [&](const Unit& un, int buf) {
+    const dma::i32x4 rs = dma::rsrc((uintptr_t)(a.x + (size_t)un.img * a.hv * w3));  // per image: 32-bit offsets
+    const long f00 = (long)(un.w0 - 4) * 3;
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
-      const uint4 af = *reinterpret_cast<const uint4*>(at + (wave * 64 + f * 16 + frow) * ALD + fk * 8);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc[f][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        Mma<bf16>::run(acc[f][j], af, bw[j]);
+    for (int q = 0; q < (XNI + 3) / 4; ++q) {
+      const int t = wave + 4 * q;
+      if (t < XNI) {
+        const int i = t * 64 + lane;
+        const int r = i / XPC, pc = i - (i / XPC) * XPC;
+        const int hh = un.h0 - 1 + r;
+        const long f0 = f00 + pc * 4;
+        const bool ok = i < (RPB + 2) * XPC && hh >= 0 && hh < a.hv && f0 >= 0 && f0 < w3;
+        dma::lds16(ok ? (unsigned)(((long)hh * w3 + f0) * 4) : dma::OOB, rs, (const char*)(xs[buf] + t * 256));
       }
     }
-    __syncthreads();  // the A tile is consumed: it becomes the C tile
-#pragma unroll
-    for (int f = 0; f < 4; ++f)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int px = wave * 64 + f * 16 + fk * 4 + r;
-          float v = acc[f][j][r] + bj[j];
-          if (relu) v = fmaxf(v, 0.f);
-          if (aff) v = v * sj[j] + hj[j];
-          const float vs = px < npx ? v : 0.f;
-          s1[j] += vs;
-          s2[j] += vs * vs;
-          at[px * ALD + j * 16 + frow] = from_f32<bf16>(v);
-        }
+  };
+  const int nis = (XNI - wave + 3) / 4;  // instructions per unit issued by this wave
+  long u = blockIdx.x;
+  int buf = 0;
+  if (u < a.units) issue(unit(u), 0);
+  for (; u < a.units; u += G) {
+    const Unit un = unit(u);
+    const int npx = min(SEG, a.w - un.w0), nrow = min(RPB, a.h - un.h0);
+    __syncthreads();  // the other buffer's previous unit is consumed
+    const bool more = u + G < a.units;
+    if (more) issue(unit(u + G), buf ^ 1);
+    dma::wait_vm_dyn(more ? nis : 0);  // this unit's pieces (and older stores) have landed
     __syncthreads();
-    const long prow = ((long)n * a.h + h0 + rr) * a.w + w0;
-    for (int i = tid; i < npx * 4; i += 256) {
-      const int px = i >> 2, pc = i & 3;
-      *reinterpret_cast<uint4*>(a.out + (prow + px) * a.out_ld + a.out_off + pc * 8) =
-          *reinterpret_cast<const uint4*>(at + px * ALD + pc * 8);
+    const float* X = xs[buf];
+    if (w3 & 3) {  // the piece at the right frame edge carries the next row's first floats
+      const int e = w3 - (int)((long)(un.w0 - 4) * 3);  // first float index past the frame
+      if (e < XRW && tid < (RPB + 2) * (4 - (w3 & 3)))
+        const_cast<float*>(X)[(tid / (4 - (w3 & 3))) * XRW + e + tid % (4 - (w3 & 3))] = 0.f;
+      __syncthreads();
     }
-    __syncthreads();
+    const int p0 = wave * 64;  // the wave's first pixel of the segment
+    if (p0 < npx) {
+#pragma unroll 1
+      for (int rr = 0; rr < nrow; ++rr) {
+        const long prow = ((long)un.img * a.h + un.h0 + rr) * a.w + un.w0;
+        const float* src = X + rr * XRW + kb + (p0 + pxl + 3) * 3;
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          bf16x8 xb;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xb[e] = from_f32<bf16>(src[f * 48 + koff[e]]);
+          const uint4 xf = __builtin_bit_cast(uint4, xb);
+          f32x4 acc[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            Mma<bf16>::run(acc[j], bw[j], xf);  // C^T: lanes = pixels
+          }
+          const int px = p0 + f * 16 + pxl;
+          const bool ok = px < npx;
+          float v[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            float t = acc[k >> 2][k & 3] + bj[k];
+            if (relu) t = fmaxf(t, 0.f);
+            if constexpr (AFF) t = t * sj[k] + hj[k];
+            v[k] = t;
+            const float vs = ok ? t : 0.f;
+            s1[k] += vs;
+            s2[k] += vs * vs;
+          }
+          if (ok) Pack16<bf16>::store(a.out + (prow + px) * a.out_ld + a.out_off + 8 * g, v);
+        }
+      }
+    }
+    buf ^= 1;
   }
   if (stats) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      s1[j] += __shfl_xor(s1[j], 16, 64);
-      s1[j] += __shfl_xor(s1[j], 32, 64);
-      s2[j] += __shfl_xor(s2[j], 16, 64);
-      s2[j] += __shfl_xor(s2[j], 32, 64);
-      if (lane < 16) {
-        red[wave][0][j * 16 + lane] = s1[j];
-        red[wave][1][j * 16 + lane] = s2[j];
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[k] += __shfl_xor(s1[k], o, 64);
+        s2[k] += __shfl_xor(s2[k], o, 64);
+      }
+    if (pxl == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[wave][0][8 * g + k] = s1[k];
+        red[wave][1][8 * g + k] = s2[k];
       }
     }
     __syncthreads();
@@ -159,94 +219,119 @@ __device__ __forceinline__ int tr32(int row, int col) {
   return row * 64 + ((((col >> 4) ^ (row >> 3)) & 1) << 5) + ((col & 15) << 1);
 }
 
-// One unit = one 256-pixel row segment.  The next unit's input rows and dz row are
-// loaded into registers while the current one is built and multiplied (the loads
-// are the whole cost of this layer; the MFMA work per unit is 16 instructions).
+// Persistent weight gradient: unit = one 256-pixel row segment; its dz row (as
+// [pixel][32] rows, trswz-swizzled by the DMA's source addressing) and its three
+// input rows (the forward's fp32 image) are LDS-DMA'd double-buffered, the next
+// unit's in flight under the current one.  Wave w reduces pixels 64w .. 64w+63:
+// dz^T fragments by ds_read_b64_tr_b16, column fragments (8 pixels of one k) built
+// from the fp32 image in registers; one [32][32] fp32 slab per workgroup.
+constexpr int WDP = SEG * 4;                // dz pieces per unit (16 B = 8 channels)
+constexpr int WXP = 3 * XPC;                // image pieces per unit (3 rows)
+constexpr int WXI = (WXP + 63) / 64;        // image DMA instructions (10)
+constexpr int WNI = WDP / 64 + WXI;         // DMA instructions per unit (26)
+constexpr int WBUF = WDP * 16 + WXI * 1024; // bytes per LDS buffer
+constexpr int WG_GRID = 768;                // persistent workgroups (3 per CU: 2 x 26 KB LDS each)
+
 __global__ __launch_bounds__(256) void conv_c3_wgrad_kernel(const float* __restrict__ x, int n, int hv, int h,
                                                             int w, int segs, const bf16* __restrict__ dz,
-                                                            long units, long per_block, float* __restrict__ slabs) {
-  constexpr int PWC = (SEG + 2) * 3, XN = (3 * PWC + 255) / 256;
-  __shared__ float xs[3 * PWC];
-  __shared__ __attribute__((aligned(16))) char Ds[SEG * 64];
-  __shared__ __attribute__((aligned(16))) char Cs[SEG * 64];
+                                                            long units, float* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * WBUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  const long G = gridDim.x;
+  const int w3 = w * 3;
   (void)n;
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const long u0 = (long)blockIdx.x * per_block, u1 = min(u0 + per_block, units);
-  float xr[XN];
-  uint4 dr[4];
-  auto load = [&](long u) {
-    const int seg = (int)(u % segs);
-    const long row = u / segs;  // img * h + oh
-    const int img = (int)(row / h), oh = (int)(row % h);
-    const int w0 = seg * SEG, npx = min(SEG, w - w0);
+  // the lane's column k = 16j + li of the image: (r, s, c) offset (k >= 27: any finite value)
+  int kof[2];
 #pragma unroll
-    for (int q = 0; q < XN; ++q) {
-      const int i = tid + q * 256;
-      const int r = i / PWC, c = i - r * PWC;
-      const int hh = oh - 1 + r, ww = w0 - 1 + c / 3;
-      xr[q] = (i < 3 * PWC && hh >= 0 && hh < hv && ww >= 0 && ww < w)
-                  ? x[(((long)img * hv + hh) * w + ww) * 3 + c % 3] : 0.f;
-    }
-    if (tid < npx) {
-      const uint4* src = reinterpret_cast<const uint4*>(dz + ((size_t)row * w + w0 + tid) * 32);
+  for (int j = 0; j < 2; ++j) {
+    const int k = 16 * j + li;
+    kof[j] = k < 27 ? (k / 9) * XRW + ((k % 9) / 3) * 3 + k % 3 : 0;
+  }
+  struct Unit {
+    int img, oh, w0;
+  };
+  auto unit = [&](long u) {
+    const long row = u / segs;
+    return Unit{(int)(row / h), (int)(row % h), (int)(u % segs) * SEG};
+  };
+  auto issue = [&](const Unit& un, int buf) {
+    char* B = lds + buf * WBUF;
+    const dma::i32x4 zs = dma::rsrc((uintptr_t)(dz + ((size_t)un.img * h + un.oh) * w * 32));
+    const dma::i32x4 xr = dma::rsrc((uintptr_t)(x + (size_t)un.img * hv * w3));
+    const long f00 = (long)(un.w0 - 4) * 3;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) dr[q] = src[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dr[q] = uint4{0u, 0u, 0u, 0u};
+    for (int q = 0; q < (WNI + 3) / 4; ++q) {
+      const int T = wave + 4 * q;
+      if (T < WDP / 64) {  // dz: LDS row = pixel, 16-byte piece pc holds logical piece pc ^ swz
+        const int row = T * 16 + (lane >> 2), pc = lane & 3;
+        const int lp = pc ^ (((row >> 3) & 1) << 1);
+        const bool ok = un.w0 + row < w;
+        dma::lds16(ok ? (unsigned)(((un.w0 + row) * 32 + lp * 8) * 2) : dma::OOB, zs, B + T * 1024);
+      } else if (T < WNI) {  // image rows oh-1 .. oh+1
+        const int t = T - WDP / 64, i = t * 64 + lane;
+        const int r = i / XPC, pc = i - (i / XPC) * XPC;
+        const int hh = un.oh - 1 + r;
+        const long f0 = f00 + pc * 4;
+        const bool ok = i < WXP && hh >= 0 && hh < hv && f0 >= 0 && f0 < w3;
+        dma::lds16(ok ? (unsigned)(((long)hh * w3 + f0) * 4) : dma::OOB, xr, B + WDP * 16 + t * 1024);
+      }
     }
   };
-  if (u0 < u1) load(u0);
-  for (long u = u0; u < u1; ++u) {
-    const int npx = min(SEG, w - (int)(u % segs) * SEG);
-#pragma unroll
-    for (int q = 0; q < XN; ++q)
-      if (tid + q * 256 < 3 * PWC) xs[tid + q * 256] = xr[q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) *reinterpret_cast<uint4*>(Ds + tr32(tid, q * 8)) = dr[q];
-    if (u + 1 < u1) load(u + 1);  // in flight under this unit's work
+  const int nis = (WNI - wave + 3) / 4;
+  long u = blockIdx.x;
+  int buf = 0;
+  if (u < units) issue(unit(u), 0);
+  for (; u < units; u += G) {
+    const Unit un = unit(u);
+    const int npx = min(SEG, w - un.w0);
     __syncthreads();
-    {
-      float v[32];
-      patch(xs, 0, tid, v);
-      if (tid >= npx) {
-#pragma unroll
-        for (int k = 0; k < 32; ++k) v[k] = 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Pack16<bf16>::store(reinterpret_cast<bf16*>(Cs + tr32(tid, q * 8)), v + q * 8);
+    const bool more = u + G < units;
+    if (more) issue(unit(u + G), buf ^ 1);
+    dma::wait_vm_dyn(more ? nis : 0);
+    __syncthreads();
+    const char* Ds = lds + buf * WBUF;
+    const float* X = reinterpret_cast<const float*>(Ds + WDP * 16);
+    if (w3 & 3) {  // the piece at the right frame edge carries the next row's first floats
+      const int e = w3 - (un.w0 - 4) * 3;
+      if (e < XRW && tid < 3 * (4 - (w3 & 3)))
+        const_cast<float*>(X)[(tid / (4 - (w3 & 3))) * XRW + e + tid % (4 - (w3 & 3))] = 0.f;
+      __syncthreads();
     }
-    __syncthreads();
+    if (wave * 64 < npx) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int r0 = wave * 64 + ks * 32 + 8 * g + qq;
-      bf16x8 af[2], bfr[2];
+      for (int ks = 0; ks < 2; ++ks) {
+        const int r0 = wave * 64 + ks * 32 + 8 * g + qq;
+        const int pb = wave * 64 + ks * 32 + 8 * g + 3;  // the lane's first pixel in the image (+3: w0-4 origin, s=0 at -1)
+        bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = i * 16 + 4 * pp;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + tr32(r0, col)));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + tr32(r0 + 4, col)));
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        const s16x4 lo2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Cs + tr32(r0, col)));
-        const s16x4 hi2 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Cs + tr32(r0 + 4, col)));
-        bfr[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo2, hi2, 0, 1, 2, 3, 4, 5, 6, 7));
+        for (int i = 0; i < 2; ++i) {
+          const int col = i * 16 + 4 * pp;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + tr32(r0, col)));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, Ds + tr32(r0 + 4, col)));
+          af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float* src = X + kof[j] + pb * 3;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bfr[j][e] = from_f32<bf16>(src[3 * e]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
+    buf ^= 1;
   }
-  // per-wave 32x32 partials -> LDS (reusing Ds/Cs as fp32 [4][32][32]) -> slab
-  float* part = reinterpret_cast<float*>(Ds);
+  __syncthreads();  // every DMA has landed (the last unit waited for all) and every read is done
+  float* part = reinterpret_cast<float*>(lds);
   const int fk = lane >> 4, frow = lane & 15;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -278,12 +363,13 @@ __global__ __launch_bounds__(256) void conv_c3_wgrad_fold_kernel(const float* __
   }
 }
 
-constexpr int WG_BLOCKS = 1024;
 
 }  // namespace
 
+static long c3_units(int n, int h, int w) { return (long)n * ((h + RPB - 1) / RPB) * ((w + SEG - 1) / SEG); }
+
 extern "C" long cnnitmo_conv_c3_stat_rows(int n, int h, int w) {
-  return (long)n * ((h + RPB - 1) / RPB) * ((w + SEG - 1) / SEG);
+  return std::min<long>(c3_units(n, h, w), C3_GRID);
 }
 
 extern "C" int cnnitmo_conv_c3_fwd(const float* x, int n, int h_valid, int h, int w, const void* wt,
@@ -294,21 +380,25 @@ extern "C" int cnnitmo_conv_c3_fwd(const float* x, int n, int h_valid, int h, in
   CNN_REQUIRE(out_ld % 8 == 0 && out_off % 8 == 0 && out_ld >= out_off + 32, "conv_c3_fwd: output view");
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || stat_part, "conv_c3_fwd: STATS without buffer");
   CNN_REQUIRE(!(flags & CNNITMO_AFFINE) || (aff_scale && aff_shift), "conv_c3_fwd: AFFINE without coefficients");
-  C3Fwd a;
+  C3Fwd2 a;
   a.x = x; a.n = n; a.hv = h_valid; a.h = h; a.w = w;
   a.segs = (w + SEG - 1) / SEG;
   a.rpn = (h + RPB - 1) / RPB;
+  a.units = c3_units(n, h, w);
   a.wt = (const bf16*)wt; a.bias = bias; a.out = (bf16*)out; a.out_ld = out_ld; a.out_off = out_off;
   a.flags = flags; a.aff_scale = aff_scale; a.aff_shift = aff_shift; a.stats = stat_part;
+  CNN_REQUIRE((long)h_valid * w * 3 < (1L << 29), "conv_c3_fwd: frame too large for 32-bit offsets");
   const long blocks = cnnitmo_conv_c3_stat_rows(n, h, w);
-  CNN_REQUIRE(blocks < (1L << 31), "conv_c3_fwd: too large");
-  hipLaunchKernelGGL(conv_c3_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  if (flags & CNNITMO_AFFINE)
+    hipLaunchKernelGGL(conv_c3_fwd_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(conv_c3_fwd_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
   return cnnitmo_check_launch("conv_c3_fwd");
 }
 
 extern "C" size_t cnnitmo_conv_c3_wgrad_workspace_bytes(int n, int h, int w) {
   (void)n; (void)h; (void)w;
-  return (size_t)WG_BLOCKS * 1024 * sizeof(float);
+  return (size_t)WG_GRID * 1024 * sizeof(float);
 }
 
 extern "C" int cnnitmo_conv_c3_wgrad(const float* x, int n, int h_valid, int h, int w, const void* dz, float* dw,
@@ -318,11 +408,11 @@ extern "C" int cnnitmo_conv_c3_wgrad(const float* x, int n, int h_valid, int h, 
   CNN_REQUIRE(ws_bytes >= cnnitmo_conv_c3_wgrad_workspace_bytes(n, h, w), "conv_c3_wgrad: workspace too small");
   const int segs = (w + SEG - 1) / SEG;
   const long units = (long)n * h * segs;
-  const long per = (units + WG_BLOCKS - 1) / WG_BLOCKS;
-  const int blocks = (int)((units + per - 1) / per);
+  CNN_REQUIRE((long)h_valid * w * 3 < (1L << 29) && (long)w * 64 < (1L << 31), "conv_c3_wgrad: frame too large");
+  const int blocks = (int)std::min<long>(units, WG_GRID);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(conv_c3_wgrad_kernel, dim3(blocks), dim3(256), 0, s, x, n, h_valid, h, w, segs,
-                     (const bf16*)dz, units, per, (float*)workspace);
+                     (const bf16*)dz, units, (float*)workspace);
   hipLaunchKernelGGL(conv_c3_wgrad_fold_kernel, dim3(32), dim3(256), 0, s, (const float*)workspace, blocks, dw);
   return cnnitmo_check_launch("conv_c3_wgrad");
 }

@@ -78,6 +78,7 @@ struct WHCfg {
   static constexpr int SMEM = ((XS + 1) * XB + DS * DB) * 1024;  // + one all-zero x row
   static constexpr int LX = (XB + NW - 1) / NW, LD = (DB + NW - 1) / NW;  // max DMA per wave per row
   static_assert(TW * BM * 2 % 1024 == 0, "dz rows must be whole KB");
+  static_assert(D >= R, "a step multiplies R rows, so at least R groups must be in flight at its wait");
   static_assert(SMEM <= 160 * 1024, "LDS");
 };
 
@@ -308,11 +309,13 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 // results): no s_barrier -11 %, no vmcnt wait -11 %, no row DMA -15 %, none of the
 // three -24 % (1.15 -> 1.5 PF/s: the MFMA + fragment-read loop alone); prefetching 4
 // rows ahead instead of 2 changed nothing.  So the 64 x 96 block (one workgroup per CU
-// at any ring size) multiplies three rows per wait + barrier, 2 groups ahead (144 KB;
-// dec6-dec9 23.02 vs 23.27 ms at two rows / 3 ahead, profiles/r03g_ab_wgrad_rows.txt);
-// the smaller blocks keep one row per step (two workgroups per CU).
+// at any ring size) multiplies two rows per wait + barrier with three groups ahead
+// (152 KB).  Three rows per step would need three groups ahead (D >= R), 165 KB: over
+// the LDS.  (profiles/r03g_ab_wgrad_rows.txt timed R3/D2, which violates D >= R: its
+// third row read a slot not yet loaded; the parity tests caught it.)  The smaller
+// blocks keep one row per step (two workgroups per CU).
 #ifndef WH_ROWS96
-#define WH_ROWS96 3
+#define WH_ROWS96 2
 #endif
 #ifndef WH_ROWS_SMALL
 #define WH_ROWS_SMALL 1
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 constexpr int wh_rows(int bm, int bn) { return bm == 64 && bn == 96 ? WH_ROWS96 : WH_ROWS_SMALL; }
 // row groups issued ahead
 #ifndef WH_AHEAD96
-#define WH_AHEAD96 2
+#define WH_AHEAD96 3
 #endif
 constexpr int wh_ahead(int r) { return r == WH_ROWS96 && WH_ROWS96 > 1 ? WH_AHEAD96 : 2; }
 

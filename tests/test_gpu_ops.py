@@ -228,7 +228,8 @@ def test_first_layer_im2col(dt):
     close(host(dw).reshape(dw_ref.shape), dw_ref, dt, "first layer wgrad")
 
 
-@pytest.mark.parametrize("N,Hv,H,W,ld,off", [(2, 13, 16, 10, 32, 0), (1, 6, 7, 300, 96, 64), (3, 9, 9, 256, 32, 0)])
+@pytest.mark.parametrize("N,Hv,H,W,ld,off", [(2, 13, 16, 10, 32, 0), (1, 6, 7, 300, 96, 64), (3, 9, 9, 256, 32, 0),
+                                             (2, 5, 6, 517, 32, 0)])
 def test_first_layer_direct(N, Hv, H, W, ld, off):
     """cnnitmo_conv_c3_fwd / _wgrad (bf16, no im2col buffer) vs the oracle: ReLU + BN
     partial sums + output view, partial 256-pixel segments, zero rows >= Hv, and a
