@@ -141,6 +141,15 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   // Every load is unconditional (pointer / index selects, no branch), which keeps the
   // compiler's vmcnt counting exact: with conditional loads it waited for all of them
   // at every unrolled group (vmcnt(0)).  nks % TWS_PD == 0 (ws_plan).
+  // BN partial sums of the lane's pixels for its 8 columns of each fragment pair, kept
+  // in registers for the whole launch (one DPP reduction at the end instead of one per
+  // tile: the per-tile reduction was as much VALU issue as the tile's MFMAs)
+  constexpr int FP = FN / 2;
+  float s1[MODE == 0 ? FP : 1][8], s2[MODE == 0 ? FP : 1][8];
+#pragma unroll
+  for (int q = 0; q < (MODE == 0 ? FP : 1); ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s1[q][k] = s2[q][k] = 0.f;
   uint4 Ab[TWS_PD][2];
   const bf16* abc[2];
   const bf16* abn[2];
@@ -184,8 +193,6 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
     // epilogue from registers: fragment pair (2q, 2q+1) gives the lane 8 consecutive
     // columns n .. n+7 of its pixel (pair_perm) -> one 16-byte store per (pixel, pair)
     // (8-byte stores, one per fragment, took 40 % of up8's forward: store-issue-bound)
-    constexpr int FP = FN / 2;
-    float s1[MODE == 0 ? FP : 1][8], s2[MODE == 0 ? FP : 1][8];
 #pragma unroll
     for (int q = 0; q < FP; ++q) {
       const int n = nb * BN + q * 32 + kq * 8;  // first of the lane's 8 columns (8 | cout)
@@ -199,8 +206,6 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
         Pack16<float>::load(par + BN + cl + 4, sj + 4);
         Pack16<float>::load(par + 2 * BN + cl, hj);
         Pack16<float>::load(par + 2 * BN + cl + 4, hj + 4);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s1[q][k] = s2[q][k] = 0.f;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           const bool ok = px[f] < P;
@@ -232,24 +237,20 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
         }
       }
     }
-    if constexpr (MODE == 0) {
-      if (stats) {
-#pragma unroll
-        for (int q = 0; q < FP; ++q)
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float a1 = row16_sum(s1[q][k]), a2 = row16_sum(s2[q][k]);
-            if (frow == 0) {
-              const int c = q * 32 + kq * 8 + k;
-              sl[c * 2] += a1;
-              sl[c * 2 + 1] += a2;
-            }
-          }
-      }
-    }
   }
   if constexpr (MODE == 0) {
     if (stats) {  // one row per wave: row = (group, wave), columns of this block
+#pragma unroll
+      for (int q = 0; q < FP; ++q)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a1 = row16_sum(s1[q][k]), a2 = row16_sum(s2[q][k]);
+          if (frow == 0) {
+            const int c = q * 32 + kq * 8 + k;
+            sl[c * 2] = a1;
+            sl[c * 2 + 1] = a2;
+          }
+        }
       __syncthreads();
       const long row = (long)gidx * NW + wave;
       for (int q = lane; q < BN; q += 64) {
@@ -334,10 +335,10 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
   const int grid = 8 * pl.gpx * pl.nblk;  // 256: one workgroup per CU
   const size_t lds = (size_t)pl.bn * (t.K * 2 + WS_PAD) + (size_t)NW * pl.bn * 2 * sizeof(float) + 3 * pl.bn * sizeof(float);
   static bool attr = [] {  // dynamic LDS beyond 64 KB
-    hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;

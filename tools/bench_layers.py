@@ -66,8 +66,9 @@ def main():
             bias = torch.zeros(cout, device="cuda", dtype=torch.float32)
             out = ops.new_view(B, 2 * hi, 2 * wi, cout, T)
             fl = 2.0 * B * hi * wi * 4 * cout * cin
-            if "fwd" in want:
-                rows.append((name, "fwd", fl, timeit(lambda: ops.tconv_fwd(dt, x, k, bias, out, 1), a.iters)))
+            if "fwd" in want:  # ReLU + BN partial sums, as in the training step
+                st = torch.empty(ops.tconv_stat_rows(dt, B, hi, wi, cin, cout) * 2 * 4 * cout, device="cuda")
+                rows.append((name, "fwd", fl, timeit(lambda: ops.tconv_fwd(dt, x, k, bias, out, 1 | 2, stats=st), a.iters)))
             if "dgrad" in want:
                 dx = torch.empty(B * hi * wi * cin, dtype=T, device="cuda")
                 rows.append((name, "dgrad", fl, timeit(lambda: ops.tconv_dgrad(dt, out.buf, B, hi, wi, cout, kT, cin, dx), a.iters)))
