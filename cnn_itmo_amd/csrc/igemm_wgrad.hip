@@ -301,16 +301,45 @@ __device__ __forceinline__ float fold_v(const WFold& f, int row, int col) {
 }
 
 // Sum the split slabs: out[row*cols_out + c] = sum_s ws[s][row*cols_in + c]
-// (then the folded-BN correction when f.mode != 0).
-__global__ void slab_reduce_kernel(const float* __restrict__ ws, long slab, int splits, int rows,
-                                   int cols_in, int cols_out, float* __restrict__ out, WFold f) {
+// (then the folded-BN correction when f.mode != 0).  A workgroup owns E consecutive
+// outputs; its S wave groups sum contiguous slab ranges (four loads in flight per
+// lane), and group 0 adds the S partials in order: the same fixed order on every run.
+// (One thread per output summing every slab in sequence was latency-bound: 0.1-0.4 ms
+// per launch at 36-500 slabs, 1.5 ms per step.)
+template <int E, int S>
+__global__ __launch_bounds__(E * S) void slab_reduce_kernel(const float* __restrict__ ws, long slab, int splits,
+                                                            int rows, int cols_in, int cols_out,
+                                                            float* __restrict__ out, WFold f) {
+  __shared__ float part[S][E];
+  const int e = threadIdx.x % E, g = threadIdx.x / E;
   const long total = (long)rows * cols_out;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const int row = (int)(i / cols_out), c = (int)(i - (long)row * cols_out);
-    const long src = (long)row * cols_in + c;
-    float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += ws[(size_t)k * slab + src];
+  const long i = (long)blockIdx.x * E + e;
+  const bool ok = i < total;
+  const int row = ok ? (int)(i / cols_out) : 0, c = ok ? (int)(i - (long)row * cols_out) : 0;
+  const long src = (long)row * cols_in + c;
+  const int per = (splits + S - 1) / S, k0 = g * per, k1 = min(k0 + per, splits);
+  float s = 0.f;
+  if (ok) {
+    int k = k0;
+    for (; k + 4 <= k1; k += 4) {
+      const float a0 = ws[(size_t)k * slab + src], a1 = ws[(size_t)(k + 1) * slab + src];
+      const float a2 = ws[(size_t)(k + 2) * slab + src], a3 = ws[(size_t)(k + 3) * slab + src];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; k < k1; ++k) s += ws[(size_t)k * slab + src];
+  }
+  if constexpr (S > 1) {
+    part[g][e] = s;
+    __syncthreads();
+    if (g == 0) {
+#pragma unroll
+      for (int q = 1; q < S; ++q) s += part[q][e];
+    }
+  }
+  if (g == 0 && ok) {
     if (f.raw) f.raw[i] = s;
     if (f.mode) {
       const int ci = c % f.cin;
@@ -318,6 +347,20 @@ __global__ void slab_reduce_kernel(const float* __restrict__ ws, long slab, int 
     }
     out[i] = s;
   }
+}
+
+// launch of slab_reduce_kernel over rows x cols_out outputs: more slab groups per
+// output when there are many slabs and few outputs
+static void slab_reduce(const float* ws, long slab, int splits, int rows, int cols_in, int cols_out, float* out,
+                        const WFold& f, hipStream_t s) {
+  const long total = (long)rows * cols_out;
+#define SRL(E, S)                                                                                              \
+  hipLaunchKernelGGL((slab_reduce_kernel<E, S>), dim3((unsigned)((total + E - 1) / E)), dim3(E * S), 0, s, ws, \
+                     slab, splits, rows, cols_in, cols_out, out, f)
+  if (splits >= 64) SRL(64, 16);
+  else if (splits >= 8) SRL(64, 4);
+  else SRL(256, 1);
+#undef SRL
 }
 
 // ----------------------------------------------------------------------------
@@ -399,15 +442,12 @@ int run_wgrad(WgradArgs a, float* out_final, int rows, int cols_in, int cols_out
   a.P = (long)a.nimg * a.hg * a.wg;
   CNN_REQUIRE(a.P > 0, "%s: empty", what);
   const long slab = (long)a.M * a.N * a.ntaps;
-  const long outn = (long)rows * cols_out;
-  const int rblocks = (int)std::min<long>((outn + 255) / 256, 4096);
   if constexpr (std::is_same<T, bf16>::value) {
     const int splits = try_wgrad2(a, tapdep, ws, ws_bytes, s);
     if (splits > 0) {
       int rc = cnnitmo_check_launch(what);
       if (rc) return rc;
-      hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)ws, slab,
-                         splits, rows, cols_in, cols_out, out_final, fold);
+      slab_reduce((const float*)ws, slab, splits, rows, cols_in, cols_out, out_final, fold, s);
       return cnnitmo_check_launch(what);
     }
   }
@@ -424,8 +464,7 @@ int run_wgrad(WgradArgs a, float* out_final, int rows, int cols_in, int cols_out
   launch_any<T>(a, pl.bm, pl.bn, s, dim3((unsigned)total));
   int rc = cnnitmo_check_launch(what);
   if (rc) return rc;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)ws, slab,
-                     pl.splits, rows, cols_in, cols_out, out_final, fold);
+  slab_reduce((const float*)ws, slab, pl.splits, rows, cols_in, cols_out, out_final, fold, s);
   return cnnitmo_check_launch(what);
 }
 
@@ -493,10 +532,8 @@ extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld,
     if (splits > 0) {
       int rc = cnnitmo_check_launch("conv_wgrad");
       if (rc) return rc;
-      const long slab = (long)cout * 9 * cin, outn = slab;
-      const int rblocks = (int)std::min<long>((outn + 255) / 256, 4096);
-      hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)workspace, slab,
-                         splits, cout, 9 * cin, cols_out, dw, f);
+      const long slab = (long)cout * 9 * cin;
+      slab_reduce((const float*)workspace, slab, splits, cout, 9 * cin, cols_out, dw, f, s);
       return cnnitmo_check_launch("conv_wgrad");
     }
   }
@@ -532,9 +569,7 @@ extern "C" int cnnitmo_conv_wgrad_cat(int dtype, const void* x1, int x1_ld, int 
   int rc = cnnitmo_check_launch("conv_wgrad_cat");
   if (rc) return rc;
   const long slab = (long)cout * 9 * cin;
-  const int rblocks = (int)std::min<long>((slab + 255) / 256, 4096);
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)workspace, slab, splits, cout,
-                     9 * cin, 9 * cin, dw, f);
+  slab_reduce((const float*)workspace, slab, splits, cout, 9 * cin, 9 * cin, dw, f, s);
   return cnnitmo_check_launch("conv_wgrad_cat");
 }
 
@@ -569,9 +604,7 @@ extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout
       int rc = cnnitmo_check_launch("tconv2x2_wgrad");
       if (rc) return rc;
       const long slab = 4L * cout * cin;
-      const int rblocks = (int)std::min<long>((slab + 255) / 256, 4096);
-      hipLaunchKernelGGL(slab_reduce_kernel, dim3(rblocks), dim3(256), 0, s, (const float*)workspace, slab,
-                         splits, 4 * cout, cin, cin, dk, f);
+      slab_reduce((const float*)workspace, slab, splits, 4 * cout, cin, cin, dk, f, s);
       return cnnitmo_check_launch("tconv2x2_wgrad");
     }
   }
