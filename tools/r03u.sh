@@ -4,6 +4,6 @@
 set -e
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 bash "$R/tools/pmc_traffic.sh"
-bash "$R/tools/profile_round.sh" r03q --steps 5 --warmup 2 --infer-batch 0 --ns-batch 0 --k4-batch 0
+bash "$R/tools/profile_round.sh" r03u --steps 5 --warmup 2 --infer-batch 0 --ns-batch 0 --k4-batch 0
 cd "$R"
-timeout -k 10 600 python3 bench.py > gpurun_out/r03q_bench.json 2> gpurun_out/r03q_bench.err
+timeout -k 10 600 python3 bench.py > gpurun_out/r03u_bench.json 2> gpurun_out/r03u_bench.err
