@@ -320,12 +320,41 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
 #ifndef WH_ROWS_SMALL
 #define WH_ROWS_SMALL 1
 #endif
-constexpr int wh_rows(int bm, int bn) { return bm == 64 && bn == 96 ? WH_ROWS96 : WH_ROWS_SMALL; }
-// row groups issued ahead
+#ifndef WH_ROWS64
+#define WH_ROWS64 2
+#endif
+constexpr int wh_rows(int bm, int bn) {
+  return bm == 64 && bn >= 96 ? WH_ROWS96 : (bm == 64 && bn == 64 ? WH_ROWS64 : WH_ROWS_SMALL);
+}
+// row groups issued ahead (64 x 128: two, the most that fits beside its 17 KB x rows)
 #ifndef WH_AHEAD96
 #define WH_AHEAD96 3
 #endif
-constexpr int wh_ahead(int r) { return r == WH_ROWS96 && WH_ROWS96 > 1 ? WH_AHEAD96 : 2; }
+constexpr int wh_ahead(int bn, int r) { return r > 1 ? (bn == 128 ? 2 : WH_AHEAD96) : 2; }
+
+template <int BM, int BN, int TW>
+int wh_occupancy() {  // resident workgroups per CU (registers AND LDS), from the runtime
+  static int occ = [] {
+    constexpr int WM = BN == 128 ? 1 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1)),
+                  WN = BN == 128 ? 4 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2));
+    constexpr int R = wh_rows(BM, BN), D = wh_ahead(BN, R);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R, false>,
+                                                     3 * WM * WN * 64, 0) != hipSuccess || n < 1)
+      n = 1;
+    return n;
+  }();
+  return occ;
+}
+
+int wh_occupancy(int bm, int bn, int tw) {
+#define WO(BMv, BNv, TWv) \
+  if (bm == BMv && bn == BNv && tw == TWv) return wh_occupancy<BMv, BNv, TWv>();
+  WO(64, 128, 64) WO(64, 96, 64) WO(64, 64, 64) WO(64, 32, 64) WO(32, 96, 64) WO(32, 64, 64) WO(32, 32, 64)
+  WO(64, 32, 128) WO(32, 64, 128) WO(32, 32, 128)
+#undef WO
+  return 1;
+}
 
 struct WHPlan {
   int bm, bn, tw, strips, cbm, cbn, rsplits, smem;
@@ -339,7 +368,12 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
   }();
   if (!mode) return false;
   pl.bm = cout % 64 == 0 ? 64 : (cout == 32 ? 32 : 0);
+  static const int bn128 = [] {
+    const char* e = getenv("CNNITMO_WH_BN128");
+    return e ? atoi(e) : 2;
+  }();
   pl.bn = cin % 96 == 0 ? 96 : (cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0));
+  if (!cat && cout % 64 == 0 && cin % 128 == 0 && (bn128 >= 2 || (bn128 == 1 && pl.bn != 96))) pl.bn = 128;
   if (!pl.bm || !pl.bn) return false;
   // 128-column strips also when w % 128 != 0 (a partial last strip): enc2a at 960
   // columns 1.12 -> 0.99 ms (tools/ab_env.sh); CNNITMO_WH_TW128=0 restores 64
@@ -367,9 +401,14 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
   const int xb = cat ? ((pl.tw + 2) * 64 + 1023) / 1024 + ((pl.tw + 2) * (pl.bn - 32) * 2 + 1023) / 1024
                      : ((pl.tw + 2) * pl.bn * 2 + 1023) / 1024,
             db = pl.tw * pl.bm * 2 / 1024;
-  const int R = wh_rows(pl.bm, pl.bn), D = wh_ahead(R);
+  const int R = wh_rows(pl.bm, pl.bn), D = wh_ahead(pl.bn, R);
   const int smem = ((D + R + 3) * xb + (D + R) * db) * 1024;  // WHCfg::SMEM
-  const int occ = std::max(1, (160 * 1024) / smem);
+#ifndef WH_OCC_API
+#define WH_OCC_API 1
+#endif
+  // workgroups per CU: the runtime's occupancy (the 64 x 64 block fits two by LDS but
+  // one by registers: 12 waves at 114 VGPRs)
+  const int occ = WH_OCC_API && !cat ? wh_occupancy(pl.bm, pl.bn, pl.tw) : std::max(1, (160 * 1024) / smem);
   const long slots = (long)ncu * occ;
   long best = 1;
   double best_eff = -1.0;
@@ -388,8 +427,11 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
 template <int BM, int BN, int TW, bool CAT = false>
 void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
   // 12 waves (3 per SIMD) for the big blocks, 6 for the small ones
-  constexpr int WM = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1), WN = BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2);
-  constexpr int R = wh_rows(BM, BN), D = wh_ahead(R);
+  // 64 x 128: 1 x 4 waves per kernel row (each 64 x 32: fewer fragment reads per MFMA than
+  // 2 x 2, and 2 x 2's 32 x 64 tiles spilled at 168 VGPRs)
+  constexpr int WM = BN == 128 ? 1 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1)),
+                WN = BN == 128 ? 4 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2));
+  constexpr int R = wh_rows(BM, BN), D = wh_ahead(BN, R);
   hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R, CAT>), dim3(grid), dim3(3 * WM * WN * 64), 0, s,
                      a);
 }
@@ -428,7 +470,7 @@ int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n
   }
 #define WH(BMv, BNv, TWv) \
   if (pl.bm == BMv && pl.bn == BNv && pl.tw == TWv) { wh_launch<BMv, BNv, TWv>(a, grid, s); return pl.strips * pl.rsplits; }
-  WH(64, 96, 64) WH(64, 64, 64) WH(64, 32, 64) WH(32, 96, 64) WH(32, 64, 64) WH(32, 32, 64)
+  WH(64, 128, 64) WH(64, 96, 64) WH(64, 64, 64) WH(64, 32, 64) WH(32, 96, 64) WH(32, 64, 64) WH(32, 32, 64)
   WH(64, 32, 128) WH(32, 64, 128) WH(32, 32, 128)
 #undef WH
   return -1;

@@ -48,7 +48,9 @@ def close(got, want, dt, what=""):
                                           # whole 4x64 tiles: the halo kernel (bf16) for fwd and dgrad
                                           (32, 32, 8, 64), (96, 64, 4, 128), (192, 128, 4, 64),
                                           (64, 64, 12, 64), (32, 64, 12, 192), (96, 64, 16, 128),
-                                          (192, 128, 8, 64), (64, 64, 16, 64), (32, 64, 24, 192)])
+                                          (192, 128, 8, 64), (64, 64, 16, 64), (32, 64, 24, 192),
+                                          # 128-channel-deep wgrad blocks, a partial last strip
+                                          (128, 64, 6, 64), (256, 128, 10, 70)])
 def test_conv3x3_fwd_dgrad_wgrad(dt, cin, cout, H, W):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(cin + cout)
