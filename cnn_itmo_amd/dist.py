@@ -33,6 +33,12 @@ import torch
 import torch.distributed as dist
 
 
+def _force():
+    """CNNITMO_DIST_FORCE=1: run the collectives even in a one-rank group (a box with
+    one GPU can then execute the RCCL path end to end: tools/rccl_world1.py)."""
+    return os.environ.get("CNNITMO_DIST_FORCE") == "1"
+
+
 def init_from_env(backend=None):
     """Initialise the default process group from torchrun-style env vars.
     Returns (rank, world, local_rank)."""
@@ -44,7 +50,7 @@ def init_from_env(backend=None):
     if os.environ.get("CNNITMO_DEVICE") is not None:
         local = int(os.environ["CNNITMO_DEVICE"])
     backend = backend or os.environ.get("CNNITMO_DIST_BACKEND") or None
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or _force()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -93,6 +99,7 @@ class GradBucketer:
         self.stats = stats
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.collect = self.world > 1 or (_force() and dist.is_initialized())
         order = sorted((r for r in stage_ranges if r[1] > r[0]), key=lambda r: r[0])
         self.buckets = make_buckets(order, int(bucket_mb * (1 << 20) / 4))
         self.timing = False      # record the compute stream's exposed wait in finish()
@@ -106,12 +113,12 @@ class GradBucketer:
         self.stat_work = None
 
     def _launch(self, lo, hi):
-        if self.world > 1:
+        if self.collect:
             self.works.append(dist.all_reduce(self.grads[lo:hi], group=self.group, async_op=True))
 
     def on_forward(self):
         """Engine callback after the forward pass: the moving statistics are final."""
-        if self.world > 1 and self.stats is not None and self.stats.numel():
+        if self.collect and self.stats is not None and self.stats.numel():
             self.stat_work = dist.all_reduce(self.stats, group=self.group, async_op=True)
 
     def hook(self, lo, hi):
@@ -169,7 +176,7 @@ def broadcast_state(engine, src=0, group=None):
 def attach(engine, bucket_mb=16.0, group=None, broadcast=True):
     """Wire a GradBucketer into an Engine; returns it.  Use
     ``engine.train_step(..., sync=b.finish, grad_scale=b.grad_scale)``."""
-    if broadcast and dist.is_initialized() and dist.get_world_size(group) > 1:
+    if broadcast and dist.is_initialized() and (dist.get_world_size(group) > 1 or _force()):
         broadcast_state(engine, group=group)
     b = GradBucketer(engine.grads, engine.stage_goff[::-1], bucket_mb, group, stats=engine.bufs)
     engine.grad_hook = b.hook

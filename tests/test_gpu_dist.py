@@ -9,8 +9,11 @@ during backward.
 * ``bench.py --gpus 2`` must start its two ranks by itself (no torchrun
   environment), report ``n_gpus == 2`` / ``dp2`` and identical replicas.
 
-(RCCL itself needs one GPU per rank: the driver's multi-GPU bench exercises it; the
-``nccl`` backend stays the default in dist.init_from_env.)"""
+RCCL refuses two ranks on one GPU, so on this box the RCCL path runs as a one-rank
+``nccl`` group with CNNITMO_DIST_FORCE=1 (``tools/rccl_world1.py``): the broadcast,
+the bucketed all-reduces launched during backward and the moving-statistics
+all-reduce execute in RCCL, and the result must be bit-identical to training without
+collectives.  The driver's multi-GPU bench runs it across GPUs."""
 import json
 import os
 import subprocess
@@ -60,3 +63,17 @@ def test_bench_spawns_ranks():
     assert res["fp32_infer"]["config"]["global_batch"] == 2
     assert res["fp32_infer_b32"]["config"]["global_batch"] == 4
     assert res["k4_train"]["config"]["global_batch"] == 2 and res["k4_train"]["config"]["parallelism"] == "dp2"
+
+
+def test_rccl_one_rank_fit_generator():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    port = str(29900 + os.getpid() % 90)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", port, os.path.join(ROOT, "tools", "rccl_world1.py")]
+    env = dict(os.environ, CNNITMO_DIST_FORCE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("CNNITMO_DIST_BACKEND", None)
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("bit-identical") == 2, r.stdout
+    print(r.stdout.strip())
