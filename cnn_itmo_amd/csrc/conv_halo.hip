@@ -64,6 +64,9 @@ constexpr int NPI = (PPC + NWAVE - 1) / NWAVE;                    // patch piece
 // taps over which the next item's DMA pieces are issued (3 and 8 measured no better,
 // profiles/r02l_ab_halo_knobs.txt)
 constexpr int PFT = 5;
+#ifndef HALO_LINES
+#define HALO_LINES 0
+#endif
 // tap offset of the DMA issue window for waves NWAVE/2.. (the second wave on each SIMD):
 // the two waves of a SIMD then issue their pieces in different taps
 #ifndef HALO_PFT_OFF
@@ -328,13 +331,19 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     return __builtin_bit_cast(dma::i32x4, o);
   };
 
-  // EPI 0 / 1: stores through a buffer descriptor at the wave's first pixel
+  // EPI 0 / 1: stores through a buffer descriptor at the wave's first pixel.  HALO_LINES
+  // (BN 64): the two column pairs of a fragment go out as whole 128-byte lines, 8 pixels
+  // per store instruction (line_pair), instead of 16 pixels x 64 bytes per instruction:
+  // parity-green but neutral on enc2b/dec6/dec8/dec9 (profiles/r03z_ab_halo_lines.txt;
+  // the halo conv's stores are a small share of its time), so off by default.
+  constexpr bool LINES = HALO_LINES && FP == 2;
   auto epilogue = [&](const Pos& e) {
     const int oh0 = e.y0 + wave * RPW;
     const bf16* obase = (const bf16*)p.out + (((size_t)e.img * p.ho + oh0) * p.wo + e.x0) * p.out_ld + p.out_off + n0;
     const __amdgpu_buffer_rsrc_t os = dma::brsrc(obase);
     const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE;
     const bool bt = EPI == 1 && p.border && (oh0 == 0 || oh0 + RPW >= p.ho || e.x0 == 0 || e.x0 + TW >= p.wo);
+    dma::i32x4 pk[LINES ? FP : 1][LINES ? FM : 1];
 #pragma unroll
     for (int q = 0; q < FP; ++q) {
       const int cl = 32 * q + 8 * g;  // the lane's first column in the block
@@ -374,8 +383,28 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
             sb[q][k] += vs * vs;
           }
         }
-        const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 2);
-        __builtin_amdgcn_raw_buffer_store_b128(pack8(v), os, ok ? off : OOB, 0, 0);
+        if constexpr (LINES) {
+          pk[q][f] = pack8(v);
+        } else {
+          const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 2);
+          __builtin_amdgcn_raw_buffer_store_b128(pack8(v), os, ok ? off : OOB, 0, 0);
+        }
+      }
+    }
+    if constexpr (LINES) {
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        uint4 v1, v2;
+        line_pair(__builtin_bit_cast(uint4, pk[0][f]), __builtin_bit_cast(uint4, pk[1][f]), pxl, v1, v2);
+        const int rr = f / FMR, c1 = (f % FMR) * 16 + (pxl & 7), c2 = c1 + 8;
+        const int cl = 32 * (pxl >> 3) + 8 * g;
+        const bool rok = oh0 + rr < p.ho;
+        const unsigned o1 = (unsigned)((((long)rr * p.wo + c1) * p.out_ld + cl) * 2);
+        const unsigned o2 = (unsigned)((((long)rr * p.wo + c2) * p.out_ld + cl) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, v1), os,
+                                               rok && e.x0 + c1 < p.wo ? o1 : OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, v2), os,
+                                               rok && e.x0 + c2 < p.wo ? o2 : OOB, 0, 0);
       }
     }
     zero_acc();

@@ -71,6 +71,24 @@ __host__ __device__ constexpr int pair_perm(int nn) {
   return 32 * (nn >> 5) + 8 * ((nn & 15) >> 2) + 4 * ((nn >> 4) & 1) + (nn & 3);
 }
 
+// Whole 128-byte lines from that layout.  Lane (frow = lane & 15, g = lane >> 4) holds
+// octet g of pixel frow for the column pairs q (a) and q + 1 (b): 64 contiguous bytes
+// of each pixel per pair, so a plain store instruction writes 16 pixels x 64 B.  After
+// one exchange with lane frow ^ 8 (DPP row_ror:8), store 1 writes pixels 0-7 and store 2
+// pixels 8-15 of the fragment, each as 8 whole lines: lane (frow, g) stores octet g of
+// pair q + (frow >> 3) of pixel (frow & 7) (v1) and of pixel 8 + (frow & 7) (v2).
+__device__ __forceinline__ void line_pair(const uint4& a, const uint4& b, int frow, uint4& v1, uint4& v2) {
+  const bool lo = frow < 8;
+  const uint4 x = lo ? b : a;  // what the partner lane needs from this one
+  uint4 y;
+  y.x = __builtin_amdgcn_update_dpp(0, (int)x.x, 0x128, 0xF, 0xF, false);
+  y.y = __builtin_amdgcn_update_dpp(0, (int)x.y, 0x128, 0xF, 0xF, false);
+  y.z = __builtin_amdgcn_update_dpp(0, (int)x.z, 0x128, 0xF, 0xF, false);
+  y.w = __builtin_amdgcn_update_dpp(0, (int)x.w, 0x128, 0xF, 0xF, false);
+  v1 = lo ? a : y;
+  v2 = lo ? y : b;
+}
+
 template <typename T> struct Mma;
 template <> struct Mma<bf16> {
   static __device__ __forceinline__ void run(f32x4& acc, const uint4& a, const uint4& b) {

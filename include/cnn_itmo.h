@@ -191,7 +191,8 @@ int cnnitmo_conv_c3_wgrad(const float* x, int n, int h_valid, int h, int w, cons
  * Conv2DTranspose(f, 2, strides=2, 'valid') -- replaces model.py:200
  * (ConvBNTranspose).  x [n,h,w,cin] contiguous; k: [2][2][cout][cin] dtype;
  * out view [n,2h,2w,cout] (ld, off); flags/stat_part as conv3x3 (stat_part
- * columns are [4*cout] = (tap, channel)).
+ * columns are [4*cout] = (tap, channel) groups; only a channel's total over the
+ * four groups is defined: cnnitmo_bn_fwd_finalize with groups = 4 folds them).
  */
 int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int w, int cin, const void* k,
                          const float* bias, int cout, void* out, int out_ld, int out_off,

@@ -418,9 +418,12 @@ class LaunchChecker(ElementwiseChecks):
                         sa2[t] += (z * z).sum((0, 1))
         acc.done()
         if stats is not None and flags & L.STATS:
-            tot = stats.view(-1, 2, 4, cout).to(F64).sum(0)
-            self._sums(lab + " stats", tot[0], s1, sa)
-            self._sums(lab + " stats^2", tot[1], s2, sa2)
+            # contract: per-channel totals over the 4 tap column groups (bn_fwd_finalize
+            # folds the groups; tconv_ws's 256-column block puts both of its taps' sums in
+            # the first tap's columns)
+            tot = stats.view(-1, 2, 4, cout).to(F64).sum(0).sum(1)
+            self._sums(lab + " stats", tot[0], s1.sum(0), sa.sum(0))
+            self._sums(lab + " stats^2", tot[1], s2.sum(0), sa2.sum(0))
 
     @staticmethod
     def _tdgrad(d6i, kt):
