@@ -442,8 +442,9 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
   static thread_local char buf[96];
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
   if (!use_v1() && fwd2_handles(a.N)) {
-    const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
-    const int bm = fwd2_bm(a, dtype == CNNITMO_BF16);
+    const bool t256 = fwd2_t256(a, dtype == CNNITMO_BF16);
+    const int bn = t256 ? 256 : a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
+    const int bm = t256 ? 256 : fwd2_bm(a, dtype == CNNITMO_BF16);
     snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,%dx%d>", t, bm, bn);
   } else {
     const Cfg c = pick_cfg(a.N);

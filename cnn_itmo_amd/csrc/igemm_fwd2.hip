@@ -341,6 +341,18 @@ int fwd2_bm(const FwdArgs& a, bool bf16) {
 }
 bool fwd2_handles(int N) { return N != 32; }
 
+// bf16 Conv2DTranspose input gradient (K = 1024 / 2048): 256 x 256 tiles (8 waves of
+// 128 x 64, 2-deep 128 KB ring, one workgroup per CU) move half the LDS-DMA bytes per
+// MFMA of the 128 x 128 tiles: up6 / up7 0.83 / 1.80 -> 0.70 / 1.66 ms
+// (profiles/r03z_ab_fwd2_256.txt); CNNITMO_FWD2_256=0 restores 128 x 128
+bool fwd2_t256(const FwdArgs& a, bool bf16) {
+  static const int en = [] {
+    const char* e = getenv("CNNITMO_FWD2_256");
+    return e ? atoi(e) : 1;
+  }();
+  return en && bf16 && a.ntaps == 4 && a.scale == 2 && a.N % 256 == 0 && !a.stats;
+}
+
 template <typename T>
 int launch_fwd2(FwdArgs a, hipStream_t s, const char* what) {
   constexpr int VE = Vec16<T>::N;
@@ -351,16 +363,8 @@ int launch_fwd2(FwdArgs a, hipStream_t s, const char* what) {
   CNN_REQUIRE(!a.scatter || a.cout % VE == 0, "%s: scatter needs cout %% %d == 0", what, VE);
   CNN_REQUIRE(a.M > 0 && a.ntaps >= 1 && a.ntaps <= 9, "%s: bad sizes", what);
   const Cfg2 c = pick2(a.N);
-  static const int t256 = [] {
-    const char* e = getenv("CNNITMO_FWD2_256");
-    return e ? atoi(e) : 1;
-  }();
-  // bf16 Conv2DTranspose input gradient (K = 1024 / 2048): 256 x 256 tiles (8 waves of
-  // 128 x 64, 2-deep 128 KB ring, one workgroup per CU) move half the LDS-DMA bytes per
-  // MFMA of the 128 x 128 tiles: up6 / up7 0.83 / 1.80 -> 0.70 / 1.66 ms
-  // (profiles/r03z_ab_fwd2_256.txt); CNNITMO_FWD2_256=0 restores 128 x 128
   if constexpr (sizeof(T) == 2) {
-    if (t256 && a.ntaps == 4 && a.scale == 2 && a.N % 256 == 0 && !a.stats) {
+    if (fwd2_t256(a, true)) {
       a.mblocks = (int)((a.M + 255) / 256);
       a.nblocks = a.N / 256;
       CNN_REQUIRE((long)a.mblocks * a.nblocks < (1L << 31), "%s: grid too large", what);
