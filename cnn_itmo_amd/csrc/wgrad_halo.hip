@@ -330,14 +330,39 @@ constexpr int wh_rows(int bm, int bn) {
 #ifndef WH_AHEAD96
 #define WH_AHEAD96 3
 #endif
-constexpr int wh_ahead(int bn, int r) { return r > 1 ? (bn == 128 ? 2 : WH_AHEAD96) : 2; }
+// the 32 x 32 block on 64-pixel strips (enc1b, HBM-bound): more row groups in flight
+#ifndef WH_AHEAD_SMALL
+#define WH_AHEAD_SMALL 2
+#endif
+constexpr int wh_ahead(int bm, int bn, int tw, int r) {
+  return r > 1 ? (bn == 128 ? 2 : WH_AHEAD96) : (bm * bn <= 32 * 32 && tw == 64 ? WH_AHEAD_SMALL : 2);
+}
+
+// waves per kernel row (WM x WN over the BM x BN block).  64 x 128: 1 x 4 (each 64 x 32:
+// fewer fragment reads per MFMA than 2 x 2, and 2 x 2's 32 x 64 tiles spilled at 168
+// VGPRs).  32 x 32 (enc1b): one wave per kernel row over the whole block (1 x 2 read 10
+// fragments per 6 MFMAs, 1 x 1 16 per 12): 2.14 -> 1.74 ms (profiles/r03zf_ab_enc1b_wn1.txt).
+// 64 x 32 (enc2a): WH_WM6432 waves down the 64 output channels (1: 0.89 -> 0.91 ms,
+// r03zg_ab_enc2a_wm1.txt, so 2).  More row groups in flight for the 32 x 32 block
+// (WH_AHEAD_SMALL 4 / 6 on 64-pixel strips) measured no faster (r03ze_ab_enc1b_wgrad.txt).
+#ifndef WH_WN32
+#define WH_WN32 1
+#endif
+#ifndef WH_WM6432
+#define WH_WM6432 2
+#endif
+constexpr int wh_wm(int bm, int bn) {
+  return bn == 128 ? 1 : (bm * bn >= 64 * 64 ? 2 : (bm >= 64 ? (bn == 32 ? WH_WM6432 : 2) : 1));
+}
+constexpr int wh_wn(int bm, int bn) {
+  return bn == 128 ? 4 : (bm * bn >= 64 * 64 ? 2 : (bm >= 64 ? 1 : (bm == 32 && bn == 32 ? WH_WN32 : 2)));
+}
 
 template <int BM, int BN, int TW>
 int wh_occupancy() {  // resident workgroups per CU (registers AND LDS), from the runtime
   static int occ = [] {
-    constexpr int WM = BN == 128 ? 1 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1)),
-                  WN = BN == 128 ? 4 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2));
-    constexpr int R = wh_rows(BM, BN), D = wh_ahead(BN, R);
+    constexpr int WM = wh_wm(BM, BN), WN = wh_wn(BM, BN);
+    constexpr int R = wh_rows(BM, BN), D = wh_ahead(BM, BN, TW, R);
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, (const void*)wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R, false>,
                                                      3 * WM * WN * 64, 0) != hipSuccess || n < 1)
@@ -401,7 +426,7 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
   const int xb = cat ? ((pl.tw + 2) * 64 + 1023) / 1024 + ((pl.tw + 2) * (pl.bn - 32) * 2 + 1023) / 1024
                      : ((pl.tw + 2) * pl.bn * 2 + 1023) / 1024,
             db = pl.tw * pl.bm * 2 / 1024;
-  const int R = wh_rows(pl.bm, pl.bn), D = wh_ahead(pl.bn, R);
+  const int R = wh_rows(pl.bm, pl.bn), D = wh_ahead(pl.bm, pl.bn, pl.tw, R);
   const int smem = ((D + R + 3) * xb + (D + R) * db) * 1024;  // WHCfg::SMEM
 #ifndef WH_OCC_API
 #define WH_OCC_API 1
@@ -426,12 +451,9 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
 
 template <int BM, int BN, int TW, bool CAT = false>
 void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
-  // 12 waves (3 per SIMD) for the big blocks, 6 for the small ones
-  // 64 x 128: 1 x 4 waves per kernel row (each 64 x 32: fewer fragment reads per MFMA than
-  // 2 x 2, and 2 x 2's 32 x 64 tiles spilled at 168 VGPRs)
-  constexpr int WM = BN == 128 ? 1 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 2 : 1)),
-                WN = BN == 128 ? 4 : (BM * BN >= 64 * 64 ? 2 : (BM >= 64 ? 1 : 2));
-  constexpr int R = wh_rows(BM, BN), D = wh_ahead(BN, R);
+  // 12 waves (3 per SIMD) for the big blocks, 6 (or 3) for the small ones
+  constexpr int WM = wh_wm(BM, BN), WN = wh_wn(BM, BN);
+  constexpr int R = wh_rows(BM, BN), D = wh_ahead(BM, BN, TW, R);
   hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, TW, WM, WN, D, R, CAT>), dim3(grid), dim3(3 * WM * WN * 64), 0, s,
                      a);
 }
