@@ -1,6 +1,7 @@
 // 3x3 'same' convolution, forward and input-gradient, bf16: every U-Net 3x3
 // layer from enc1b on (model.py:196 Conv2D(filters, 3, padding='same') -> ReLU
-// -> BatchNormalization, and its input gradient).
+// -> BatchNormalization, and its input gradient); and the fp32 inference forward
+// (predict.py:62 at fp32) with 16-channel chunks.
 //
 // GEMM view: rows = output pixels, columns = output channels (N), K = 9 taps x
 // Cin.  A workgroup owns a 16 x 32 output tile and a block of BN columns.  Per
@@ -106,10 +107,19 @@ struct HaloArgs {
   long tiles;
 };
 
-template <int BN, int EPI, bool RES>
+// TE = bf16 (every launch of the training step) or float (the fp32 inference forward,
+// EPI 1 only).  An LDS row is 64 B either way: CC = 32 bf16 or 16 fp32 channels per
+// chunk, and one 16-byte piece is PE = 8 or 4 channels; Mma<float> runs a 16-byte
+// fragment as four 16x16x4 f32 MFMAs, so the fragment reads, the swizzle and the
+// operand-swapped register layout are the same.  fp32 stores take two 16-byte stores per
+// (pixel, 8 channels).
+template <typename TE, int BN, int EPI, bool RES>
 __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   using C = HCfg<BN, RES>;
   constexpr int FN = C::FN, FP = C::FP, L = C::L, NBI = C::NBI, STAGE = C::STAGE, ST = C::ST;
+  constexpr int ES = sizeof(TE), CC = 64 / ES, PE = 16 / ES;
+  constexpr int NST = C::NST * (ES == 4 ? 2 : 1);  // stores per wave per epilogue
+  static_assert(ES == 2 || EPI == 1, "fp32: the forward epilogue only");
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -129,8 +139,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   const int n0 = nb * BN;
   const int K = KT * p.cin;
   const int tpi = h.tiles_x * h.tiles_y;
-  const bf16* __restrict__ X = (const bf16*)p.a;
-  const bf16* __restrict__ Wt = (const bf16*)p.b;
+  const TE* __restrict__ X = (const TE*)p.a;
+  const TE* __restrict__ Wt = (const TE*)p.b;
   float* par = reinterpret_cast<float*>(smem + C::PAR);
   float* utb = reinterpret_cast<float*>(smem + C::UTB);
   // the workgroup's epilogue parameters (ordered before any epilogue by the ring barrier)
@@ -191,10 +201,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     ppy[i] = row < PROWS ? py - 1 : -(1 << 29);  // padding rows: never in bounds
     ppx[i] = px - 1;
     pkey[i] = EPI == 1 ? (unsigned)((py * p.ws + px) * 4 + piece)
-                       : (unsigned)((((long)py * p.ws + px) * p.a_ld + piece * 8) * 2);
+                       : (unsigned)((((long)py * p.ws + px) * p.a_ld + piece * PE) * ES);
   }
   // the source of a chunk: a (channels < cin1 or a single source) or a2
-  const bf16* __restrict__ X2 = (const bf16*)p.a2;
+  const TE* __restrict__ X2 = (const TE*)p.a2;
   const int cin1 = p.a2 ? p.cin1 : p.cin;
   unsigned boff[NBI];
 #pragma unroll
@@ -202,7 +212,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const int row = (wave * NBI + i) * 16 + lrow;  // = tap * BN + nn
     const int piece = lpc ^ (((row >> 2) & 1) << 1);
     const int tap = row / BN, nn = row - (row / BN) * BN;
-    boff[i] = row < KT * BN ? (unsigned)((pair_perm(nn) * K + tap * p.cin + piece * 8) * 2) : OOB;
+    boff[i] = row < KT * BN ? (unsigned)((pair_perm(nn) * K + tap * p.cin + piece * PE) * ES) : OOB;
   }
   uintptr_t pbase = 0, bbase = 0;
   char* iPs = smem;
@@ -211,21 +221,21 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const Pos& s = ip;
     iPs = smem + buf * STAGE;
     const long po = ((long)s.img * p.hs + s.y0 - 1) * p.ws + s.x0 - 1;  // patch origin pixel (may be < 0)
-    const int c = s.ch * 32;
+    const int c = s.ch * CC;
     bbase = (uintptr_t)(Wt + (size_t)n0 * K + c);
     if constexpr (EPI == 1) {
       const bool second = c >= cin1;
       const long ld = second ? p.a2_ld : p.a_ld;
-      pbase = second ? (uintptr_t)X2 + (uintptr_t)((po * ld + p.a2_off + c - cin1) * 2)
-                     : (uintptr_t)X + (uintptr_t)((po * ld + p.a_off + c) * 2);
+      pbase = second ? (uintptr_t)X2 + (uintptr_t)((po * ld + p.a2_off + c - cin1) * ES)
+                     : (uintptr_t)X + (uintptr_t)((po * ld + p.a_off + c) * ES);
 #pragma unroll
       for (int i = 0; i < NPI; ++i) {
         const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
         const bool ok = (unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws;
-        pvo[i] = ok ? ((pkey[i] >> 2) * (unsigned)ld + (pkey[i] & 3) * 8) * 2 : OOB;
+        pvo[i] = ok ? ((pkey[i] >> 2) * (unsigned)ld + (pkey[i] & 3) * PE) * ES : OOB;
       }
     } else {
-      pbase = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + c) * 2);
+      pbase = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + c) * ES);
 #pragma unroll
       for (int i = 0; i < NPI; ++i) {
         const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
@@ -301,7 +311,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], bfr[cur][j], af[cur][i]);  // C^T: lanes = pixels
+        for (int j = 0; j < FN; ++j) Mma<TE>::run(acc[i][j], bfr[cur][j], af[cur][i]);  // C^T: lanes = pixels
       if (pf) {
         const int toff = HALO_PFT_OFF && wave >= NWAVE / 2 ? HALO_PFT_OFF : 0;
 #pragma unroll
@@ -336,10 +346,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // per store instruction (line_pair), instead of 16 pixels x 64 bytes per instruction:
   // parity-green but neutral on enc2b/dec6/dec8/dec9 (profiles/r03z_ab_halo_lines.txt;
   // the halo conv's stores are a small share of its time), so off by default.
-  constexpr bool LINES = HALO_LINES && FP == 2;
+  constexpr bool LINES = HALO_LINES && FP == 2 && ES == 2;
   auto epilogue = [&](const Pos& e) {
     const int oh0 = e.y0 + wave * RPW;
-    const bf16* obase = (const bf16*)p.out + (((size_t)e.img * p.ho + oh0) * p.wo + e.x0) * p.out_ld + p.out_off + n0;
+    const TE* obase = (const TE*)p.out + (((size_t)e.img * p.ho + oh0) * p.wo + e.x0) * p.out_ld + p.out_off + n0;
     const __amdgpu_buffer_rsrc_t os = dma::brsrc(obase);
     const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE;
     const bool bt = EPI == 1 && p.border && (oh0 == 0 || oh0 + RPW >= p.ho || e.x0 == 0 || e.x0 + TW >= p.wo);
@@ -385,6 +395,11 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
         }
         if constexpr (LINES) {
           pk[q][f] = pack8(v);
+        } else if constexpr (ES == 4) {
+          const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 4);
+          const float4 lo = {v[0], v[1], v[2], v[3]}, hi = {v[4], v[5], v[6], v[7]};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, lo), os, ok ? off : OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, hi), os, ok ? off + 16 : OOB, 0, 0);
         } else {
           const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 2);
           __builtin_amdgcn_raw_buffer_store_b128(pack8(v), os, ok ? off : OOB, 0, 0);
@@ -468,7 +483,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 
   if constexpr (RES) {  // the resident weights: every chunk's pieces, then a full drain
     for (int ch = 0; ch < nch; ++ch) {
-      const uintptr_t wb = (uintptr_t)(Wt + (size_t)n0 * K + ch * 32);
+      const uintptr_t wb = (uintptr_t)(Wt + (size_t)n0 * K + ch * CC);
       char* dst = smem + C::WRES + ch * (C::BPC * 1024);
 #pragma unroll
       for (int i = 0; i < NBI; ++i) {
@@ -519,7 +534,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     if (ep.ch == nch - 1) {
       if constexpr (EPI == 2) epilogue_bnb(ep);
       else epilogue(ep);
-      issued += C::NST;
+      issued += NST;
     }
     step(ep);
 #pragma unroll
@@ -613,14 +628,27 @@ int halo_ncu() {
   return ncu;
 }
 
-// conv3x3 stride 1 'same' (forward or input-gradient), bf16, 32-channel chunks
-bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
+// conv3x3 stride 1 'same' (forward or input-gradient), 64-byte chunks (32 bf16 / 16 fp32
+// channels); fp32: the inference forward only (EPI 1 without BN sums, one source)
+bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_HALO");
     return e ? atoi(e) : 1;
   }();
-  if (!en) return false;
-  if (a.cin % 32 || a.a_ld % 8 || a.a_off % 8 || a.out_ld % 8 || a.out_off % 8) return false;
+  // fp32 inference forward: 82.9 -> 94.8 frames/s at 1080p b8, the kernel at 0.87 of fp32
+  // peak against the implicit GEMM's 0.75 (profiles/r03zl_*); CNNITMO_HALO_F32=0 restores it
+  static const int en32 = [] {
+    const char* e = getenv("CNNITMO_HALO_F32");
+    return e ? atoi(e) : 1;
+  }();
+  if (!en || (f32 && !en32)) return false;
+  if (f32) {
+    if (a.cin % 16 || a.a_ld % 4 || a.a_off % 4 || a.out_ld % 4 || a.out_off % 4) return false;
+    if (a.a2 || a.bnb_out || a.stats || (a.flags & CNNITMO_STATS)) return false;
+    if (!(a.flags || a.bias || a.border)) return false;  // EPI 1
+  } else if (a.cin % 32 || a.a_ld % 8 || a.a_off % 8 || a.out_ld % 8 || a.out_off % 8) {
+    return false;
+  }
   if (a.a2 && (a.cin1 % 32 || a.cin1 <= 0 || a.cin1 >= a.cin || a.a2_ld % 8 || a.a2_off % 8 || a.bnb_out))
     return false;
   if (a.ntaps != 9 || a.scale != 1 || a.scatter || a.hs != a.ho || a.ws != a.wo) return false;
@@ -639,33 +667,33 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl) {
     const char* e = getenv("CNNITMO_HALO_RES");
     return e ? atoi(e) : 1;
   }();
-  pl.res = res && a.cin <= 32 * RCH;
+  pl.res = res && a.cin <= (f32 ? 16 : 32) * RCH;
   return true;
 }
 
-template <int BN, int EPI>
+template <typename T, int BN, int EPI>
 void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
-  if (res) hipLaunchKernelGGL((halo_conv_kernel<BN, EPI, true>), dim3(grid), dim3(NT), 0, s, h);
-  else hipLaunchKernelGGL((halo_conv_kernel<BN, EPI, false>), dim3(grid), dim3(NT), 0, s, h);
+  if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true>), dim3(grid), dim3(NT), 0, s, h);
+  else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false>), dim3(grid), dim3(NT), 0, s, h);
 }
 
 int halo_streams(const FwdArgs& a, const HaloPlan& pl) { return halo_ncu() / (a.N / pl.bn); }
 
 }  // namespace
 
-bool halo_handles(const FwdArgs& a) {
+bool halo_handles(const FwdArgs& a, bool f32) {
   HaloPlan pl;
-  return halo_plan(a, pl);
+  return halo_plan(a, pl, f32);
 }
 
-int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
+int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
   HaloPlan pl;
-  CNN_REQUIRE(halo_plan(a, pl), "%s: no halo plan", what);
+  CNN_REQUIRE(halo_plan(a, pl, f32), "%s: no halo plan", what);
   HaloArgs h;
   h.f = a;
   h.tiles_x = (a.wo + TW - 1) / TW;  // partial edge tiles are masked
   h.tiles_y = (a.ho + TH - 1) / TH;
-  h.nchunks = a.cin / 32;
+  h.nchunks = a.cin / (f32 ? 16 : 32);
   h.tiles = (long)a.nimg * h.tiles_x * h.tiles_y;
   h.nblocks = a.N / pl.bn;
   h.streams = halo_streams(a, pl);
@@ -673,24 +701,27 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what) {
   CNN_REQUIRE(h.tiles * h.nchunks < (1L << 31), "%s: too many tiles", what);
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
   const int grid = halo_ncu();
-  if (pl.epi == 2) {
-    if (pl.bn == 64) launch_cfg<64, 2>(h, pl.res, grid, s);
-    else launch_cfg<32, 2>(h, pl.res, grid, s);
+  if (f32) {
+    if (pl.bn == 64) launch_cfg<float, 64, 1>(h, pl.res, grid, s);
+    else launch_cfg<float, 32, 1>(h, pl.res, grid, s);
+  } else if (pl.epi == 2) {
+    if (pl.bn == 64) launch_cfg<bf16, 64, 2>(h, pl.res, grid, s);
+    else launch_cfg<bf16, 32, 2>(h, pl.res, grid, s);
   } else if (pl.epi == 1) {
-    if (pl.bn == 64) launch_cfg<64, 1>(h, pl.res, grid, s);
-    else launch_cfg<32, 1>(h, pl.res, grid, s);
+    if (pl.bn == 64) launch_cfg<bf16, 64, 1>(h, pl.res, grid, s);
+    else launch_cfg<bf16, 32, 1>(h, pl.res, grid, s);
   } else {
-    if (pl.bn == 64) launch_cfg<64, 0>(h, pl.res, grid, s);
-    else launch_cfg<32, 0>(h, pl.res, grid, s);
+    if (pl.bn == 64) launch_cfg<bf16, 64, 0>(h, pl.res, grid, s);
+    else launch_cfg<bf16, 32, 0>(h, pl.res, grid, s);
   }
   return cnnitmo_check_launch(what);
 }
 
-const char* halo_name(const FwdArgs& a) {
+const char* halo_name(const FwdArgs& a, bool f32) {
   HaloPlan pl;
-  if (!halo_plan(a, pl)) return "";
+  if (!halo_plan(a, pl, f32)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "halo_conv_kernel<%d,%d%s>", pl.bn, pl.epi, pl.res ? ",wres" : "");
+  snprintf(buf, sizeof(buf), "halo_conv_kernel<%s%d,%d%s>", f32 ? "f32," : "", pl.bn, pl.epi, pl.res ? ",wres" : "");
   return buf;
 }
 

@@ -115,9 +115,9 @@ int fwd2_bm(const FwdArgs& a, bool bf16);  // row tile of the v2 launch (128 or 
 bool fwd2_t256(const FwdArgs& a, bool bf16);  // 256 x 256 tiles (bf16 tconv input gradient)
 
 // halo-tiled 3x3 conv (bf16, 4x64 output tiles), conv_halo.hip
-bool halo_handles(const FwdArgs& a);
-int launch_halo(FwdArgs a, hipStream_t s, const char* what);
-const char* halo_name(const FwdArgs& a);
+bool halo_handles(const FwdArgs& a, bool f32 = false);  // f32: the fp32 inference forward
+int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32 = false);
+const char* halo_name(const FwdArgs& a, bool f32 = false);
 long halo_stat_rows(const FwdArgs& a);
 
 // tconv_stream.hip: Conv2DTranspose fwd (mode 0) / input-gradient (mode 1) as a

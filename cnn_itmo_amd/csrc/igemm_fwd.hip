@@ -294,6 +294,7 @@ bool use_v1() {
 int dispatch(int dtype, const FwdArgs& a, void* stream, const char* what) {
   hipStream_t s = (hipStream_t)stream;
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return launch_halo(a, s, what);
+  if (dtype == CNNITMO_F32 && halo_handles(a, true)) return launch_halo(a, s, what, true);
   if (!use_v1() && fwd2_handles(a.N)) {
     if (dtype == CNNITMO_BF16) return launch_fwd2<bf16>(a, s, what);
     if (dtype == CNNITMO_F32) return launch_fwd2<float>(a, s, what);
@@ -413,6 +414,7 @@ extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int 
   if (!dgrad) a.flags = CNNITMO_RELU;  // the forward epilogue variant (every U-Net conv has one)
   static thread_local char buf[96];
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
+  if (dtype == CNNITMO_F32 && halo_handles(a, true)) return halo_name(a, true);  // (no BN sums: inference)
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
   if (!use_v1() && fwd2_handles(a.N)) {
     const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
