@@ -30,19 +30,20 @@ def unmangle(n):
     """Itanium-mangled template kernels with a bf16 (DF16b) / float first argument,
     e.g. _Z17igemm_fwd2_kernelIDF16bLi256ELi128ELi4ELi2ELi3EEv7FwdArgs (c++filt
     here does not know DF16b)."""
-    m = re.match(r"_Z\d+([A-Za-z_0-9]+?)I(DF16b|f)((?:Li\d+E)*)E", n)
+    m = re.match(r"_Z(?:N12_GLOBAL__N_1)?\d+([A-Za-z_0-9]+?)I(DF16b|f)((?:L[ib]\d+E)*)E", n)
     if not m:
         return n
     t = "__bf16" if m.group(2) == "DF16b" else "float"
-    ints = re.findall(r"Li(\d+)E", m.group(3))
-    return "%s<%s>" % (m.group(1), ",".join([t] + ints))
+    args = [("true" if v == "1" else "false") if k == "b" else v for k, v in re.findall(r"L([ib])(\d+)E", m.group(3))]
+    return "%s<%s>" % (m.group(1), ",".join([t] + args))
 
 
 def label(name):
     n = unmangle(name.replace(" ", "")).replace("(anonymousnamespace)::", "")
-    m = re.search(r"halo_conv_kernel<(\d+),(\d+)(?:,(true|false))?>", n)
+    m = re.search(r"halo_conv_kernel<(?:(__bf16|float),)?(\d+),(\d+)(?:,(true|false))?>", n)
     if m:
-        return "halo_conv_kernel<%s,%s%s>" % (m.group(1), m.group(2), ",wres" if m.group(3) == "true" else "")
+        return "halo_conv_kernel<%s%s,%s%s>" % ("f32," if m.group(1) == "float" else "", m.group(2), m.group(3),
+                                               ",wres" if m.group(4) == "true" else "")
     m = re.search(r"halo_gemm_kernel<(\d+),(\d+),(\d+),(\d+),\d+(?:,(\d+))?>", n)
     if m:
         return "halo_gemm_kernel<%s,%s,%s,%s%s>" % (m.groups()[:4] + (",bnb" if m.group(5) not in (None, "0") else "",))
