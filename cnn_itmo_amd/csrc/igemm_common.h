@@ -132,12 +132,14 @@ int launch_tconv_stream(int mode, const void* a, long a_ld, int a_off, const voi
 
 // tconv_ws.hip: Conv2DTranspose fwd (mode 0) / input-gradient (mode 1) as a
 // weight-stationary GEMM, barrier-free after the prologue (bf16; up6..up8)
-bool tconv_ws_handles(int mode, int cin, int cout);
+// (f32: the fp32 inference forward, no BN sums)
+bool tconv_ws_handles(int mode, int cin, int cout, bool f32 = false);
 long tconv_ws_rows(int cin, int cout);
-const char* tconv_ws_name(int mode, int cin, int cout);
+const char* tconv_ws_name(int mode, int cin, int cout, bool f32 = false);
 int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b, int n, int h, int w, int cin,
                     int cout, void* out, long out_ld, int out_off, const float* bias, int flags,
-                    const float* aff_scale, const float* aff_shift, float* stats, hipStream_t s, const char* what);
+                    const float* aff_scale, const float* aff_shift, float* stats, hipStream_t s, const char* what,
+                    bool f32 = false);
 
 // v2 (direct-to-LDS, multi-tap) bf16 weight gradients, igemm_wgrad2.hip
 struct Wgrad2Args {

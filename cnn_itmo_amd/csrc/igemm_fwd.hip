@@ -432,6 +432,8 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
     return tconv_stream_name(dgrad ? 1 : 0, h, w, cin, cout, false);
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout))
     return tconv_ws_name(dgrad ? 1 : 0, cin, cout);
+  if (dtype == CNNITMO_F32 && !dgrad && tconv_ws_handles(0, cin, cout, true))  // (inference: no BN sums)
+    return tconv_ws_name(0, cin, cout, true);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
   a.cin = dgrad ? cout : cin;
@@ -546,6 +548,9 @@ extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int 
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout))
     return launch_tconv_ws(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
                            aff_shift, stat_part, (hipStream_t)stream, "tconv2x2_fwd");
+  if (dtype == CNNITMO_F32 && !(flags & CNNITMO_STATS) && tconv_ws_handles(0, cin, cout, true))
+    return launch_tconv_ws(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
+                           aff_shift, nullptr, (hipStream_t)stream, "tconv2x2_fwd", true);
   return dispatch(dtype, a, stream, "tconv2x2_fwd");
 }
 

@@ -42,12 +42,12 @@ constexpr int WS_PAD = 32;
 #endif
 
 struct WSArgs {
-  const bf16* a;
+  const void* a;
   long a_ld;
   int a_off;
-  const bf16* b;  // [N][K]
+  const void* b;  // [N][K]
   int nimg, h, w, cout, K, N;
-  bf16* out;
+  void* out;
   long out_ld;
   int out_off;
   const float* bias;
@@ -70,11 +70,19 @@ __device__ __forceinline__ float row16_sum(float v) {
 // FM: 16-pixel fragment rows per wave tile (tile = 16 * FM pixels).  SQ: distinct BN-stat
 // column pairs of the block (BN / 32, or half that when the block spans two taps of the
 // same channels: BN = 2 * cout, whose pair q and q + SQ hold one channel's sums).
-template <int MODE, int BN, int NKS, int FM = 2, int SQ = BN / 32>
+// TE = float: the fp32 inference forward (MODE 0 without BN sums).  A 16-byte fragment
+// piece is KE = 8 bf16 / 4 fp32 channels, so one K-step (four lane groups) is KS = 32 / 16
+// channels and 64 bytes in either type; Mma<float> runs a fragment as four 16x16x4 MFMAs.
+template <int MODE, int BN, int NKS, int FM = 2, int SQ = BN / 32, typename TE = bf16>
 __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   constexpr int FN = BN / 16, TP = 16 * FM;
+  constexpr int ES = sizeof(TE), KE = 16 / ES, KS = 64 / ES;
+  static_assert(ES == 2 || MODE == 0, "fp32: the forward only");
+  const TE* __restrict__ PA = (const TE*)p.a;
+  const TE* __restrict__ PB = (const TE*)p.b;
+  TE* __restrict__ PO = (TE*)p.out;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int K = p.K, ldsrow = K * 2 + WS_PAD;
+  const int K = p.K, ldsrow = K * ES + WS_PAD;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int xcd = blockIdx.x & 7, i = blockIdx.x >> 3;
@@ -84,11 +92,11 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   const long t0 = gidx * per, t1 = t0 + per < p.tiles ? t0 + per : p.tiles;
   // the weight block, once; LDS row nn holds block column pair_perm(nn), so a lane's
   // fragment pair (2q, 2q+1) ends up with 8 consecutive columns (16-byte stores)
-  const int pieces = K / 8;
+  const int pieces = K / KE;
   for (int q = tid; q < BN * pieces; q += NW * 64) {
     const int row = q / pieces, pc = q - row * pieces;
     *reinterpret_cast<uint4*>(smem + row * ldsrow + pc * 16) =
-        *reinterpret_cast<const uint4*>(p.b + (size_t)(nb * BN + pair_perm(row)) * K + pc * 8);
+        *reinterpret_cast<const uint4*>(PB + (size_t)(nb * BN + pair_perm(row)) * K + pc * KE);
   }
   // the block's epilogue parameters [3][BN] (bias, affine scale, shift by true column),
   // in LDS: a global load in the epilogue would make its vmcnt wait retire the next
@@ -110,26 +118,26 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   const long P = (long)p.nimg * hw;
   const int frow = lane & 15, kq = lane >> 4;
   const char* Bl = smem + frow * ldsrow + kq * 16;
-  constexpr int nks = NKS;  // K / 32, compile-time: the K loop unrolls fully
+  constexpr int nks = NKS;  // K / KS, compile-time: the K loop unrolls fully
 
   // the lane's A row bases for tile t (its two fragment rows; clamped for a tail tile)
-  auto bases = [&](long t, const bf16** ab) {
+  auto bases = [&](long t, const TE** ab) {
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
       const long q = t * TP + f * 16 + frow, pc = q < P ? q : P - 1;
       if constexpr (MODE == 0) {
-        ab[f] = p.a + pc * p.a_ld + p.a_off + kq * 8;
+        ab[f] = PA + pc * p.a_ld + p.a_off + kq * KE;
       } else {
         const int pi = (int)pc, img = pi / hw, rem = pi - img * hw, y = rem / p.w, x = rem - y * p.w;
-        ab[f] = p.a + (((size_t)img * 2 * p.h + 2 * y) * 2 * p.w + 2 * x) * p.cout + kq * 8;
+        ab[f] = PA + (((size_t)img * 2 * p.h + 2 * y) * 2 * p.w + 2 * x) * p.cout + kq * 8;
       }
     }
   };
-  auto loadA = [&](const bf16* const* ab, int ks, uint4* dst) {
+  auto loadA = [&](const TE* const* ab, int ks, uint4* dst) {
 #pragma unroll
     for (int f = 0; f < FM; ++f) {
       if constexpr (MODE == 0) {
-        dst[f] = *reinterpret_cast<const uint4*>(ab[f] + ks * 32);
+        dst[f] = *reinterpret_cast<const uint4*>(ab[f] + ks * KS);
       } else {
         const int k0 = ks * 32, tap = k0 / p.cout, co = k0 - tap * p.cout;
         dst[f] = *reinterpret_cast<const uint4*>(ab[f] + ((tap >> 1) * 2 * p.w + (tap & 1)) * p.cout + co);
@@ -151,8 +159,8 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) s1[q][k] = s2[q][k] = 0.f;
   uint4 Ab[TWS_PD][FM];
-  const bf16* abc[FM];
-  const bf16* abn[FM];
+  const TE* abc[FM];
+  const TE* abn[FM];
   long t = t0 + wave;
   bases(t < t1 ? t : t0, abc);
 #pragma unroll
@@ -172,7 +180,7 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
       for (int j = 0; j < FN; ++j) {
         const uint4 bfr = *reinterpret_cast<const uint4*>(Bl + j * 16 * ldsrow + ks * 64);
 #pragma unroll
-        for (int f = 0; f < FM; ++f) Mma<bf16>::run(acc[f][j], bfr, a[f]);  // C^T: lanes = pixels
+        for (int f = 0; f < FM; ++f) Mma<TE>::run(acc[f][j], bfr, a[f]);  // C^T: lanes = pixels
       }
     };
 #pragma unroll
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
       for (int j = 0; j < TWS_PD; ++j) {
         const int kn = ks + j + TWS_PD - 1;
         const bool cur = kn < nks;
-        const bf16* sel[FM];
+        const TE* sel[FM];
 #pragma unroll
         for (int f = 0; f < FM; ++f) sel[f] = cur ? abc[f] : abn[f];
         loadA(sel, cur ? kn : kn - nks, Ab[(j + TWS_PD - 1) % TWS_PD]);
@@ -218,6 +226,7 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
           for (int f = 0; f < FM; ++f) {
             const bool ok = px[f] < P;
             bf16x8 o;
+            float vf[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               float v = acc[f][2 * qq + (k >> 2)][k & 3] + bj[k];
@@ -227,8 +236,19 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
               s1[qq % SQ][k] += vs;
               s2[qq % SQ][k] += vs * vs;
               o[k] = (bf16)v;
+              vf[k] = v;
             }
             pk[hq][f] = __builtin_bit_cast(uint4, o);
+            if constexpr (ES == 4) {  // fp32: 8 channels = two 16-byte stores, no line exchange
+              if (ok) {
+                const int n = nb * BN + qq * 32 + kq * 8, tap = n / p.cout, co = n - tap * p.cout;
+                const int ip = (int)px[f], img = ip / hw, rem = ip - img * hw, y = rem / p.w, x = rem - y * p.w;
+                const size_t op = ((size_t)img * 2 * p.h + 2 * y + (tap >> 1)) * 2 * p.w + 2 * x + (tap & 1);
+                float4* d = reinterpret_cast<float4*>(PO + op * p.out_ld + p.out_off + co);
+                d[0] = float4{vf[0], vf[1], vf[2], vf[3]};
+                d[1] = float4{vf[4], vf[5], vf[6], vf[7]};
+              }
+            }
           }
         } else {
 #pragma unroll
@@ -241,17 +261,18 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
         }
       }
       // destination of (pixel index pi, block column pair qq, the lane's octet)
-      auto dst = [&](long pi, int qq) -> bf16* {
+      auto dst = [&](long pi, int qq) -> TE* {
         const int n = nb * BN + qq * 32 + kq * 8;
         if constexpr (MODE == 0) {
           const int tap = n / p.cout, co = n - tap * p.cout;
           const int ip = (int)pi, img = ip / hw, rem = ip - img * hw, y = rem / p.w, x = rem - y * p.w;
           const size_t op = ((size_t)img * 2 * p.h + 2 * y + (tap >> 1)) * 2 * p.w + 2 * x + (tap & 1);
-          return p.out + op * p.out_ld + p.out_off + co;
+          return PO + op * p.out_ld + p.out_off + co;
         } else {
-          return p.out + (size_t)pi * p.out_ld + p.out_off + n;
+          return PO + (size_t)pi * p.out_ld + p.out_off + n;
         }
       };
+      if constexpr (ES == 4) continue;  // (stored above)
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
 #if TWS_LINES
@@ -301,9 +322,15 @@ struct WSPlan {
   int bn, nblk, gpx;
 };
 
-bool ws_plan(int mode, int cin, int cout, WSPlan& pl) {
+bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_TCONV_WS");
+    return e ? atoi(e) : 1;
+  }();
+  // fp32 inference forward (up6-up8): 0.61-0.69 -> 0.79-0.80 of fp32 peak, 1080p b8 fp32
+  // inference 94.3 -> 95.9 frames/s (profiles/r03zp_*); CNNITMO_TCONV_WS_F32=0 restores the GEMM
+  static const int en32 = [] {
+    const char* e = getenv("CNNITMO_TCONV_WS_F32");
     return e ? atoi(e) : 1;
   }();
   if (!en || cout % 32 || cin % 32) return false;
@@ -311,6 +338,15 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl) {
   // K = 256 or 512: the row padding below is conflict-free (K % 128 == 0) and the K loop
   // is compiled for K / 32 = 8 or 16 steps (a multiple of TWS_PD)
   if (K != 256 && K != 512) return false;
+  if (f32) {  // fp32 inference forward: the widest block whose fp32 rows fit (K 512: 64, 256: 128)
+    if (!en32 || mode != 0) return false;
+    const int bn = K == 512 ? 64 : 128;
+    if (N % bn || N / bn > 32 || 32 % (N / bn)) return false;
+    pl.bn = bn;
+    pl.nblk = N / bn;
+    pl.gpx = 32 / pl.nblk;
+    return true;
+  }
   static const int bn256 = [] {
     const char* e = getenv("CNNITMO_TWS_BN256");
     return e ? atoi(e) : 0;
@@ -345,9 +381,9 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl) {
 
 }  // namespace
 
-bool tconv_ws_handles(int mode, int cin, int cout) {
+bool tconv_ws_handles(int mode, int cin, int cout, bool f32) {
   WSPlan pl;
-  return ws_plan(mode, cin, cout, pl);
+  return ws_plan(mode, cin, cout, pl, f32);
 }
 
 // BN partial-sum rows of the forward: one per (pixel group, wave)
@@ -357,45 +393,52 @@ long tconv_ws_rows(int cin, int cout) {
   return 8L * pl.gpx * NW;
 }
 
-const char* tconv_ws_name(int mode, int cin, int cout) {
+const char* tconv_ws_name(int mode, int cin, int cout, bool f32) {
   WSPlan pl;
-  if (!ws_plan(mode, cin, cout, pl)) return "";
+  if (!ws_plan(mode, cin, cout, pl, f32)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "tconv_ws_kernel<%d,%d>", mode, pl.bn);  // (bn 256: 16-pixel wave tiles)
+  snprintf(buf, sizeof(buf), "tconv_ws_kernel<%s%d,%d>", f32 ? "f32," : "", mode, pl.bn);  // (bn 256: 16-pixel tiles)
   return buf;
 }
 
 int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b, int n, int h, int w, int cin,
                     int cout, void* out, long out_ld, int out_off, const float* bias, int flags,
-                    const float* aff_scale, const float* aff_shift, float* stats, hipStream_t s, const char* what) {
+                    const float* aff_scale, const float* aff_shift, float* stats, hipStream_t s, const char* what,
+                    bool f32) {
   WSPlan pl;
-  CNN_REQUIRE(ws_plan(mode, cin, cout, pl), "%s: no weight-stationary plan", what);
+  CNN_REQUIRE(ws_plan(mode, cin, cout, pl, f32), "%s: no weight-stationary plan", what);
+  CNN_REQUIRE(!f32 || !(flags & CNNITMO_STATS), "%s: fp32 weight-stationary forward has no BN sums", what);
   CNN_REQUIRE(a_ld % 8 == 0 && a_off % 8 == 0 && out_ld % 4 == 0 && out_off % 4 == 0, "%s: misaligned views", what);
   CNN_REQUIRE((long)n * h * w < (1L << 31), "%s: too many pixels", what);
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || (stats && mode == 0), "%s: STATS without buffer", what);
   WSArgs t;
-  t.a = (const bf16*)a; t.a_ld = a_ld; t.a_off = a_off; t.b = (const bf16*)b;
+  t.a = a; t.a_ld = a_ld; t.a_off = a_off; t.b = b;
   t.nimg = n; t.h = h; t.w = w; t.cout = cout;
   t.K = mode == 0 ? cin : 4 * cout;
   t.N = mode == 0 ? 4 * cout : cin;
-  t.out = (bf16*)out; t.out_ld = out_ld; t.out_off = out_off;
+  t.out = out; t.out_ld = out_ld; t.out_off = out_off;
   t.bias = bias; t.flags = flags; t.aff_scale = aff_scale; t.aff_shift = aff_shift; t.stats = stats;
   t.nblk = pl.nblk; t.gpx = pl.gpx;
   const int tp = pl.bn == 256 ? 16 : 32;  // pixels per wave tile
   t.tiles = ((long)n * h * w + tp - 1) / tp;
   const int grid = 8 * pl.gpx * pl.nblk;  // 256: one workgroup per CU
-  const size_t lds = (size_t)pl.bn * (t.K * 2 + WS_PAD) + 3 * pl.bn * sizeof(float);
+  const size_t lds = (size_t)pl.bn * (t.K * (f32 ? 4 : 2) + WS_PAD) + 3 * pl.bn * sizeof(float);
   static bool attr = [] {  // dynamic LDS beyond 64 KB
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 256, 8, 1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 64, 32, 2, 2, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
 #define TWL(M, KS) hipLaunchKernelGGL((tconv_ws_kernel<M, 128, KS>), dim3(grid), dim3(NW * 64), lds, s, t)
-  if (pl.bn == 256) {
+  if (f32) {  // K / 16 steps
+    if (t.K == 512) hipLaunchKernelGGL((tconv_ws_kernel<0, 64, 32, 2, 2, float>), dim3(grid), dim3(NW * 64), lds, s, t);
+    else hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 16, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
+  } else if (pl.bn == 256) {
     hipLaunchKernelGGL((tconv_ws_kernel<0, 256, 8, 1, 4>), dim3(grid), dim3(NW * 64), lds, s, t);
   } else if (mode == 0) {
     if (t.K == 256) TWL(0, 8);

@@ -30,12 +30,20 @@ def unmangle(n):
     """Itanium-mangled template kernels with a bf16 (DF16b) / float first argument,
     e.g. _Z17igemm_fwd2_kernelIDF16bLi256ELi128ELi4ELi2ELi3EEv7FwdArgs (c++filt
     here does not know DF16b)."""
-    m = re.match(r"_Z(?:N12_GLOBAL__N_1)?\d+([A-Za-z_0-9]+?)I(DF16b|f)((?:L[ib]\d+E)*)E", n)
+    m = re.match(r"_Z(?:N12_GLOBAL__N_1)?\d+([A-Za-z_0-9]+?)I((?:L[ib]\d+E|DF16b|f)+)E", n)
     if not m:
         return n
-    t = "__bf16" if m.group(2) == "DF16b" else "float"
-    args = [("true" if v == "1" else "false") if k == "b" else v for k, v in re.findall(r"L([ib])(\d+)E", m.group(3))]
-    return "%s<%s>" % (m.group(1), ",".join([t] + args))
+    args = []
+    for tok in re.findall(r"L[ib]\d+E|DF16b|f", m.group(2)):
+        if tok == "DF16b":
+            args.append("__bf16")
+        elif tok == "f":
+            args.append("float")
+        elif tok[1] == "b":
+            args.append("true" if tok[2:-1] == "1" else "false")
+        else:
+            args.append(tok[2:-1])
+    return "%s<%s>" % (m.group(1), ",".join(args))
 
 
 def label(name):
@@ -50,9 +58,9 @@ def label(name):
     m = re.search(r"tconv_stream_kernel<(\d+),(\d+),\d+,(true|false)>", n)
     if m:
         return "tconv_stream_kernel<%s,%s%s>" % (m.group(1), m.group(2), ",bnb" if m.group(3) == "true" else "")
-    m = re.search(r"tconv_ws_kernel<(\d+),(\d+)(?:,\d+)*>", n)
+    m = re.search(r"tconv_ws_kernel<(\d+),(\d+)(?:,\d+)*(?:,(__bf16|float))?>", n)
     if m:
-        return "tconv_ws_kernel<%s,%s>" % m.groups()
+        return "tconv_ws_kernel<%s%s,%s>" % ("f32," if m.group(3) == "float" else "", m.group(1), m.group(2))
     m = re.search(r"wgrad_halo_kernel<(\d+),(\d+),(\d+),", n)
     if m:
         return "wgrad_halo_kernel<%s,%s,%s>" % m.groups()
