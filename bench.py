@@ -60,7 +60,8 @@ def parse():
                     help="fp32 inference leg (configs[1]) frames per GPU; 0 = skip")
     ap.add_argument("--k4-batch", type=int, default=8,
                     help="4K bf16 training leg (configs[4]: 3840x2160, global 64 on 8 GPUs) frames per GPU; 0 = skip")
-    ap.add_argument("--k4-steps", type=int, default=4)
+    ap.add_argument("--k4-steps", type=int, default=10)
+    ap.add_argument("--k4-warmup", type=int, default=3)
     ap.add_argument("--ns-batch", type=int, default=32,
                     help="north-star leg: fp32 1080p inference (conv2d forward) at this batch per GPU; 0 = skip")
     return ap.parse_args()
@@ -274,7 +275,7 @@ def cpu_baseline(args, P_init, H, W, train=True):
             "cores": blas, "kind": "port",
             "sample": f"oracle/unet_ref.py numpy fp32 {what} on 1 frame {w}x{h} "
                       f"({frac:.4f} of a 1920x{H} frame, scaled by pixel count); {dt:.2f} s",
-            "seconds": dt, "affinity_cores": cores, "blas_threads": blas, "cpu_model": model,
+            "seconds": dt, "padded_h": H, "affinity_cores": cores, "blas_threads": blas, "cpu_model": model,
             "threads_note": THREADS_NOTE}
 
 
@@ -512,11 +513,26 @@ def main():
             cpu = {"error": repr(e)}
 
     # The secondary legs never cost the headline line: an exception (e.g. out of memory)
-    # is recorded in the leg's own field and the JSON line is still printed.
+    # is recorded in the leg's own field and the JSON line is still printed.  Under N > 1
+    # the ranks agree on each leg's outcome (a MIN all-reduce of an ok flag) before the
+    # next leg's collectives, so one rank's failure marks the leg failed on every rank
+    # instead of leaving the others blocked in a collective.  A leg's allocations (the
+    # part that can fail on one rank alone) come before its first collective, where it
+    # calls agree(ok) itself.
+    def agree(ok):
+        if world > 1:
+            f = torch.tensor([1.0 if ok else 0.0], device="cuda")
+            torch.distributed.all_reduce(f, op=torch.distributed.ReduceOp.MIN)
+            if f.item() < 1.0 and ok:
+                raise RuntimeError("leg failed on another rank")
+        return ok
+
     def guarded(fn, *a):
+        ok = True
         try:
             return fn(*a)
         except Exception as e:
+            ok = False
             import traceback
             traceback.print_exc()
             return {"error": repr(e)[:500]}
@@ -525,6 +541,10 @@ def main():
             timer.rec = []
             C.clear_session()
             torch.cuda.empty_cache()
+            try:
+                agree(ok)
+            except RuntimeError:
+                pass
 
     # configs[1]: fp32 inference leg (b8 1080p, BN moving stats), same ranks, weak
     infer = ns = k4 = None
@@ -534,13 +554,13 @@ def main():
         C.clear_session()
         torch.cuda.empty_cache()
     if args.mode == "train" and args.infer_batch > 0:
-        infer = guarded(infer_leg, args, rank, world, timer, barrier, P_init, H, W, args.infer_batch, True)
+        infer = guarded(infer_leg, args, rank, world, timer, barrier, agree, P_init, H, W, args.infer_batch, True)
     # north star: fp32 conv2d forward at 1080p batch 32 (BASELINE.json "Target: >=40% of fp32 MFMA peak")
     if args.mode == "train" and args.ns_batch > 0:
-        ns = guarded(infer_leg, args, rank, world, timer, barrier, P_init, H, W, args.ns_batch, False)
+        ns = guarded(infer_leg, args, rank, world, timer, barrier, agree, P_init, H, W, args.ns_batch, False)
     # configs[4]: 4K training (b8 per GPU = global 64 on 8 GPUs), DP when N > 1
     if args.mode == "train" and args.k4_batch > 0:
-        k4 = guarded(k4_leg, args, rank, world, barrier)
+        k4 = guarded(k4_leg, args, rank, world, timer, barrier, agree, cpu if args.mode == "train" else None)
 
     if rank == 0:
         res = "1080p" if (args.height, args.width) == (1080, 1920) else f"{args.width}x{args.height}"
@@ -570,7 +590,7 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def infer_leg(args, rank, world, timer, barrier, P_init, H, W, B, with_cpu):
+def infer_leg(args, rank, world, timer, barrier, agree, P_init, H, W, B, with_cpu):
     """BASELINE configs[1]: 1080p frames, batch B (8) per GPU, fp32, forward-only inference
     (predict.py:62 semantics: BN moving stats), through Model.predict's engine path with
     inputs resident in HBM.  Its own roofline (dominant kernel, HIP events) and CPU
@@ -578,24 +598,30 @@ def infer_leg(args, rank, world, timer, barrier, P_init, H, W, B, with_cpu):
     "fp32 conv2d fwd at 1080p batch=32" point."""
     import torch
     import cnn_itmo_amd as C
-    with contextlib.redirect_stdout(io.StringIO()):
-        m = C.U_net(input_size=(args.height, args.width, 3), pad=True, dtype="float32", seed=0, verbose=False)
-    # non-trivial moving statistics (seeded), as a trained checkpoint would hold
-    rng = np.random.default_rng(5)
-    named = {}
-    for k, v in m.named_weights().items():
-        if k.endswith("/moving_mean"):
-            named[k] = rng.uniform(0.0, 0.5, v.shape).astype(np.float32)
-        elif k.endswith("/moving_variance"):
-            named[k] = rng.uniform(0.5, 2.0, v.shape).astype(np.float32)
-    m.set_named_weights(named)
-    P = m.named_weights() if rank == 0 else None
-    eng = m._engine()
-    torch.cuda.reset_peak_memory_stats()
-    g = torch.Generator(device="cuda")
-    g.manual_seed(77 + 7919 * rank)
-    x = torch.randint(0, 256, (B, args.height, args.width, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
-    yhat = torch.empty(B, args.height, args.width, 3, device="cuda", dtype=torch.float32)
+    ok = False
+    try:  # allocations before the first collective (see main's agree)
+        with contextlib.redirect_stdout(io.StringIO()):
+            m = C.U_net(input_size=(args.height, args.width, 3), pad=True, dtype="float32", seed=0, verbose=False)
+        # non-trivial moving statistics (seeded), as a trained checkpoint would hold
+        rng = np.random.default_rng(5)
+        named = {}
+        for k, v in m.named_weights().items():
+            if k.endswith("/moving_mean"):
+                named[k] = rng.uniform(0.0, 0.5, v.shape).astype(np.float32)
+            elif k.endswith("/moving_variance"):
+                named[k] = rng.uniform(0.5, 2.0, v.shape).astype(np.float32)
+        m.set_named_weights(named)
+        P = m.named_weights() if rank == 0 else None
+        eng = m._engine()
+        torch.cuda.reset_peak_memory_stats()
+        g = torch.Generator(device="cuda")
+        g.manual_seed(77 + 7919 * rank)
+        x = torch.randint(0, 256, (B, args.height, args.width, 3), generator=g, device="cuda",
+                          dtype=torch.uint8).float() / 255.0
+        yhat = torch.empty(B, args.height, args.width, 3, device="cuda", dtype=torch.float32)
+        ok = True
+    finally:
+        agree(ok)
 
     def step():
         eng.forward(x, training=False)
@@ -653,27 +679,36 @@ def _shape(mode, h, w, b, dtype):
     return f"{mode} {h}x{w} b{b} {dtype}"
 
 
-def k4_leg(args, rank, world, barrier):
+def k4_leg(args, rank, world, timer, barrier, agree, cpu_1080):
     """BASELINE configs[4]: 3840x2160 frames, bf16, fwd+bwd+RMSprop, k4_batch frames per
     GPU (8 = global 64 on 8 GPUs), DP over the same ranks when N > 1.  The activations
     are not tiled: at 8 frames per GPU the step's working set fits one GPU's HBM
     (peak_mem_gib), so the frame is processed whole, which keeps every pixel's
-    receptive field exact."""
+    receptive field exact.  Same two passes as the headline: K timed
+    steps without instrumentation, then min(K, 10) steps with every conv launch
+    bracketed by HIP events (roofline of the dominant kernel, PMC traffic of the
+    profiled 4K shape).  cpu_baseline: the headline leg's oracle training step (one
+    960x544 crop, same run) scaled to a 3840x2160 frame by pixel count."""
     import torch
     import cnn_itmo_amd as C
     Hk, Wk = 2160, 3840
-    with contextlib.redirect_stdout(io.StringIO()):
-        m = C.U_net(input_size=(Hk, Wk, 3), pad=True, dtype="bfloat16", seed=0, verbose=False)
-    eng = m._engine()
+    B = args.k4_batch
+    ok = False
+    try:  # everything that can fail alone (allocation) happens before the first collective
+        with contextlib.redirect_stdout(io.StringIO()):
+            m = C.U_net(input_size=(Hk, Wk, 3), pad=True, dtype="bfloat16", seed=0, verbose=False)
+        eng = m._engine()
+        g = torch.Generator(device="cuda")
+        g.manual_seed(4321 + 7919 * rank)
+        x = torch.randint(0, 256, (B, Hk, Wk, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+        t = torch.randint(0, 256, (B, Hk, Wk, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
+        ok = True
+    finally:
+        agree(ok)
     dp = None
     if world > 1:
         m.distribute(bucket_mb=args.bucket_mb)
         dp = m._dp
-    B = args.k4_batch
-    g = torch.Generator(device="cuda")
-    g.manual_seed(4321 + 7919 * rank)
-    x = torch.randint(0, 256, (B, Hk, Wk, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
-    t = torch.randint(0, 256, (B, Hk, Wk, 3), generator=g, device="cuda", dtype=torch.uint8).float() / 255.0
     opt = m.optimizer
     torch.cuda.reset_peak_memory_stats()
 
@@ -683,25 +718,50 @@ def k4_leg(args, rank, world, barrier):
             kw.update(sync=dp.finish, grad_scale=dp.grad_scale)
         return eng.train_step(x, t, **kw)
 
-    for i in range(max(1, min(args.warmup, 2))):
+    def timed(n, first):
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(n):
+            out = step(first + i)
+        barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        return el.item(), out
+
+    for i in range(max(1, args.k4_warmup)):
         step(i)
     k = max(1, args.k4_steps)
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(k):
-        out = step(100 + i)
-    barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
-    if world > 1:
-        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-    elapsed = el.item()
+    elapsed, out = timed(k, 100)
     loss = out.cpu().numpy().tolist() if out is not None else None
+    timer.reset()
+    timer.on = True
+    k2 = max(1, min(k, 10))
+    elapsed2, _ = timed(k2, 200)
+    timer.on = False
+    agg = timer.summary()
+    Hp = -(-Hk // 16) * 16
+    roof, step_flops = _roofline(agg, k2, elapsed2, BF16_PEAK_TF, _shape("train", Hk, Wk, B, "bfloat16"))
+    roof["timed_pass_ms_per_step"] = round(elapsed2 / k2 * 1e3, 2)
+    if rank == 0:
+        _print_agg(agg, "k4")
+        _print_detail(timer.detail(), k2, "k4")
     res = {"metric": "4K SDR->HDR frames/sec (fwd+bwd)", "value": round(B * world * k / elapsed, 3),
-           "unit": "frames/s", "dtype": "bf16", "steps": k, "ms_per_step": round(elapsed / k * 1e3, 2),
+           "unit": "frames/s", "dtype": "bf16", "steps": k, "warmup": max(1, args.k4_warmup),
+           "ms_per_step": round(elapsed / k * 1e3, 2),
            "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1), "last_loss_acc": loss,
-           "config": {"workload": f"U-Net train step, {Wk}x{Hk} frames, {B} frames/GPU (BASELINE configs[4]; "
-                                  f"whole frames, no spatial tiling needed)", "global_batch": B * world,
-                      "parallelism": f"dp{world}"}}
+           "config": {"workload": f"U-Net train step, {Wk}x{Hk} frames padded to {Wk}x{Hp}, {B} frames/GPU "
+                                  f"(BASELINE configs[4]; whole frames, no spatial tiling needed)",
+                      "global_batch": B * world, "parallelism": f"dp{world}",
+                      "gflop_per_frame": round(step_flops / B / 1e9, 1)},
+           "roofline": roof, "cpu_baseline": None}
+    if cpu_1080 and "value" in cpu_1080:
+        sc = (1920.0 * cpu_1080["padded_h"]) / (Wk * Hp)  # 1080p-frame equivalents -> 4K frames
+        res["cpu_baseline"] = {"value": cpu_1080["value"] * sc, "unit": "4K frames/s (fwd+bwd, fp32)",
+                               "cores": cpu_1080["cores"], "kind": cpu_1080["kind"],
+                               "sample": cpu_1080["sample"] + f"; the same timing scaled to a {Wk}x{Hp} frame "
+                                                              f"by pixel count (x{sc:.4f})",
+                               "seconds": cpu_1080["seconds"], "threads_note": cpu_1080.get("threads_note")}
     del eng, m, x, t
     return res
 

@@ -128,7 +128,9 @@ __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 
         const int r = i / XPC, pc = i - (i / XPC) * XPC;
         const int hh = un.h0 - 1 + r;
         const long f0 = f00 + pc * 4;
-        const bool ok = i < (RPB + 2) * XPC && hh >= 0 && hh < a.hv && f0 >= 0 && f0 < w3;
+        // whole pieces only: the piece straddling the row end (w % 4 != 0) would read past
+        // the tensor at its last row; it lands zeros here and is patched below
+        const bool ok = i < (RPB + 2) * XPC && hh >= 0 && hh < a.hv && f0 >= 0 && f0 + 4 <= w3;
         dma::lds16(ok ? (unsigned)(((long)hh * w3 + f0) * 4) : dma::OOB, rs, (const char*)(xs[buf] + t * 256));
       }
     }
@@ -146,10 +148,13 @@ __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 
     dma::wait_vm_dyn(more ? nis : 0);  // this unit's pieces (and older stores) have landed
     __syncthreads();
     const float* X = xs[buf];
-    if (w3 & 3) {  // the piece at the right frame edge carries the next row's first floats
-      const int e = w3 - (int)((long)(un.w0 - 4) * 3);  // first float index past the frame
-      if (e < XRW && tid < (RPB + 2) * (4 - (w3 & 3)))
-        const_cast<float*>(X)[(tid / (4 - (w3 & 3))) * XRW + e + tid % (4 - (w3 & 3))] = 0.f;
+    if (w3 & 3) {  // the piece straddling the right frame edge: its nv valid floats by guarded loads
+      const int nv = w3 & 3, e0 = w3 - nv - (int)((long)(un.w0 - 4) * 3);  // its first float in the staged row
+      if (e0 < XRW && tid < (RPB + 2) * 4) {
+        const int r = tid >> 2, k = tid & 3, hh = un.h0 - 1 + r;
+        const bool ok = k < nv && hh >= 0 && hh < a.hv;
+        const_cast<float*>(X)[r * XRW + e0 + k] = ok ? a.x[((size_t)un.img * a.hv + hh) * w3 + (w3 - nv) + k] : 0.f;
+      }
       __syncthreads();
     }
     const int p0 = wave * 64;  // the wave's first pixel of the segment
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(256) void conv_c3_wgrad_kernel(const float* __restr
         const int r = i / XPC, pc = i - (i / XPC) * XPC;
         const int hh = un.oh - 1 + r;
         const long f0 = f00 + pc * 4;
-        const bool ok = i < WXP && hh >= 0 && hh < hv && f0 >= 0 && f0 < w3;
+        const bool ok = i < WXP && hh >= 0 && hh < hv && f0 >= 0 && f0 + 4 <= w3;  // (edge piece: patched)
         dma::lds16(ok ? (unsigned)(((long)hh * w3 + f0) * 4) : dma::OOB, xr, B + WDP * 16 + t * 1024);
       }
     }
@@ -297,10 +302,13 @@ __global__ __launch_bounds__(256) void conv_c3_wgrad_kernel(const float* __restr
     __syncthreads();
     const char* Ds = lds + buf * WBUF;
     const float* X = reinterpret_cast<const float*>(Ds + WDP * 16);
-    if (w3 & 3) {  // the piece at the right frame edge carries the next row's first floats
-      const int e = w3 - (un.w0 - 4) * 3;
-      if (e < XRW && tid < 3 * (4 - (w3 & 3)))
-        const_cast<float*>(X)[(tid / (4 - (w3 & 3))) * XRW + e + tid % (4 - (w3 & 3))] = 0.f;
+    if (w3 & 3) {  // the piece straddling the right frame edge: its nv valid floats by guarded loads
+      const int nv = w3 & 3, e0 = w3 - nv - (un.w0 - 4) * 3;
+      if (e0 < XRW && tid < 3 * 4) {
+        const int r = tid >> 2, k = tid & 3, hh = un.oh - 1 + r;
+        const bool ok = k < nv && hh >= 0 && hh < hv;
+        const_cast<float*>(X)[r * XRW + e0 + k] = ok ? x[((size_t)un.img * hv + hh) * w3 + (w3 - nv) + k] : 0.f;
+      }
       __syncthreads();
     }
     if (wave * 64 < npx) {

@@ -400,6 +400,18 @@ extern "C" int cnnitmo_conv3x3_fwd_cat(int dtype, const void* x1, int x1_ld, int
   return launch_halo(a, (hipStream_t)stream, "conv3x3_fwd_cat");
 }
 
+extern "C" int cnnitmo_conv3x3_fwd_cat_supported(int dtype, int n, int h, int w, int c1, int cin, int cout) {
+  if (dtype != CNNITMO_BF16 || c1 <= 0 || c1 >= cin) return 0;
+  FwdArgs a = base_args();
+  a.a = (const void*)16; a.a_ld = c1;
+  a.a2 = (const void*)16; a.a2_ld = cin - c1; a.cin1 = c1;
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cin; a.N = cout; a.M = (long)n * h * w; a.out_ld = cout; a.cout = cout;
+  a.flags = CNNITMO_RELU;  // every U-Net conv has the forward epilogue
+  return halo_handles(a) ? 1 : 0;
+}
+
 // Name of the kernel cnnitmo_conv3x3_fwd (dgrad = 0) or cnnitmo_conv3x3_dgrad
 // (dgrad = 1; cin/cout as in the layer) launches for these sizes (for profiles).
 extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int w, int cin, int cout,

@@ -165,12 +165,6 @@ class ImageDataGenerator:
         return ArrayIterator(x, y, self, batch_size, shuffle, seed, output, rank, world)
 
 
-# (tick, frames) of the latest global batch drawn by any rank-sharded iterator: lets
-# Model.fit_generator weight unequal shares exactly when the iterators reach it through
-# the reference's builtin ``zip(input, target)`` (main.py:99), which hides them.
-LAST_GLOBAL = [0, None]
-
-
 def _shard(rank, world):
     """(rank, world) for a generator: explicit values, else the initialised
     torch.distributed group, else (0, 1)."""
@@ -260,9 +254,6 @@ class Iterator:
     def __next__(self):
         blk = next(self._gen)
         self.last_global_batch = len(blk)
-        if self.world > 1:
-            LAST_GLOBAL[0] += 1
-            LAST_GLOBAL[1] = len(blk)
         return self._batch(blk)
 
     next = __next__

@@ -829,7 +829,8 @@ class Engine:
         BN-backward apply read conv1 in half lines and up9 writes them.  Its consumer
         (dec9a, a 3x3 conv) then reads both members directly: cnnitmo_conv3x3_fwd_cat /
         cnnitmo_conv_wgrad_cat (bf16 halo kernels; its input gradient is already split
-        per member).  CNNITMO_SPLIT_CAT=0: one concat buffer."""
+        per member).  CNNITMO_SPLIT_CAT=0, or sizes either entry point rejects: one
+        concat buffer."""
         if self.dt != L.BF16 or os.environ.get("CNNITMO_SPLIT_CAT", "1") == "0":
             return
         readers = {}
@@ -848,7 +849,10 @@ class Engine:
             esz = 2  # bf16
             if (c1 * esz) % 128 == 0 and (c * esz) % 128 == 0:
                 continue  # member slices already cover whole lines
-            if not ops.wgrad_cat_supported(1, v.h, v.w, c1, c, rs[0].cout):
+            # both halves must run on the split members: the forward (bf16 halo kernel,
+            # which CNNITMO_HALO=0 or a small device rules out) and the weight gradient
+            if not (ops.fwd_cat_supported(self.dt, 1, v.h, v.w, c1, c, rs[0].cout)
+                    and ops.wgrad_cat_supported(1, v.h, v.w, c1, c, rs[0].cout)):
                 continue
             v.split = True
 

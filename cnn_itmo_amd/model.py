@@ -361,11 +361,9 @@ class Model:
             t0 = time.time()
             pending = []
             for step in range(steps_per_epoch):
-                from .datagen import LAST_GLOBAL
-                tick = LAST_GLOBAL[0]
                 xb, yb = next(generator)
                 cbs.call("on_batch_begin", step, {"batch": step, "size": len(xb)})
-                la = self.train_on_batch(xb, yb, sync=False, global_batch=_global_batch(generator, tick))
+                la = self.train_on_batch(xb, yb, sync=False, global_batch=_global_batch(generator))
                 pending.append((la, len(xb)))
                 cbs.call("on_batch_end", step, {"batch": step, "size": len(xb)})
             tot = np.zeros(3)
@@ -495,16 +493,24 @@ class Model:
             self.set_named_weights({k[2:]: z[k] for k in z.files if k.startswith("w/")})
 
 
-def _global_batch(gen, tick):
+def _global_batch(gen):
     """Frames of the global batch just drawn over all ranks: the generator's own
-    ``last_global_batch`` (rank-sharded iterators, Model.fit), else the one recorded by
-    the rank-sharded iterators during this draw (the reference's builtin
-    ``zip(input, target)``, main.py:99, hides them); None if unknown."""
+    ``last_global_batch`` (rank-sharded iterators, Model.fit); for the reference's
+    builtin ``zip(input, target)`` (main.py:99), the members' values when every member
+    is a rank-sharded datagen Iterator and they agree; otherwise None (the mean of the
+    ranks' batch means).  A wrapper that prefetches or merges draws is not a zip of
+    iterators, so it never borrows a count that belongs to another batch."""
     v = getattr(gen, "last_global_batch", None)
     if v is not None:
         return v
-    from .datagen import LAST_GLOBAL
-    return LAST_GLOBAL[1] if LAST_GLOBAL[0] != tick else None
+    if type(gen) is zip:
+        from .datagen import Iterator
+        members = gen.__reduce__()[1]  # zip pickles as (zip, (iterator, ...))
+        if members and all(isinstance(m, Iterator) for m in members):
+            vals = {m.last_global_batch for m in members}
+            if len(vals) == 1:
+                return vals.pop()
+    return None
 
 
 def _dist_world():

@@ -142,6 +142,10 @@ def conv_wgrad_cat(dt, x1: View, x2: View, dz, cout, dw, fold=None, raw=None):
          stream_ptr())
 
 
+def fwd_cat_supported(dt, n, h, w, c1, cin, cout):
+    return query("cnnitmo_conv3x3_fwd_cat_supported", dt, n, h, w, c1, cin, cout) == 1
+
+
 def wgrad_cat_supported(n, h, w, c1, cin, cout):
     return query("cnnitmo_wgrad_cat_workspace_bytes", n, h, w, c1, cin, cout) > 0
 

@@ -86,6 +86,10 @@ int cnnitmo_conv3x3_fwd_cat(int dtype, const void* x1, int x1_ld, int x1_off, in
                             const float* bias, int cout, void* out, int out_ld, int out_off, int flags,
                             const float* aff_scale, const float* aff_shift, float* stat_part,
                             const float* border, void* stream);
+/* 1 if cnnitmo_conv3x3_fwd_cat runs for these sizes in this process (dtype, the
+ * channel split, CNNITMO_HALO and the device's workgroup count decide), else 0: a
+ * planner must not keep a concat split into members the forward cannot read. */
+int cnnitmo_conv3x3_fwd_cat_supported(int dtype, int n, int h, int w, int c1, int cin, int cout);
 
 /* Name of the kernel conv3x3_fwd (dgrad = 0) / conv3x3_dgrad (dgrad = 1, same
  * layer cin/cout) launches for these sizes (profiling labels; no GPU needed). */

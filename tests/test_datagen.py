@@ -184,9 +184,8 @@ def test_rank_shards_union_is_global_stream(world, nfr, bs):
         itr = gr.flow(frames, batch_size=bs, seed=5, rank=r, world=world)
         assert len(itr) == nfr // (bs * world) + (1 if nfr % (bs * world) >= world else 0)
         for b in range(nb):
-            tick = D.LAST_GLOBAL[0]
             next(itr)
-            assert itr.last_global_batch == gsz[b] and D.LAST_GLOBAL == [tick + 1, gsz[b]]
+            assert itr.last_global_batch == gsz[b]
         shards.append(cr.seen)
     for b in range(nb):
         fr, params = ref[b]
@@ -218,3 +217,35 @@ def test_rank_shards_stay_paired_and_validate():
         D.ImageDataGenerator().flow(frames, batch_size=2, seed=1, rank=2, world=2)
     with pytest.raises(ValueError):
         D.ImageDataGenerator().flow(frames[:1], batch_size=2, seed=1, rank=0, world=2)
+
+
+def test_global_batch_of_zip_and_wrappers():
+    """Model.fit_generator's global-batch count (model._global_batch): read from the
+    zip's own members when all are rank-sharded iterators that agree (main.py:99's
+    zip(input, target)); any other wrapper (a prefetching generator, a zip with a
+    foreign member, members that disagree) gets None, never another batch's count."""
+    from cnn_itmo_amd.model import _global_batch
+    frames = np.zeros((7, 8, 8, 3), np.uint8)
+
+    def flow():
+        g = D.ImageDataGenerator()
+        _Capture(g)
+        return g.flow(frames, batch_size=2, seed=1, rank=0, world=2)
+    ia, ib = flow(), flow()
+    z = zip(ia, ib)
+    sizes = []
+    for _ in range(3):
+        next(z)
+        sizes.append(_global_batch(z))
+    assert sizes == [4, 3, 4], sizes  # global batch 4 over 2 ranks; the 7-frame epoch's tail is 3
+    assert _global_batch(ia) == 4
+
+    def prefetch(it):
+        yield from it
+    assert _global_batch(prefetch(zip(flow(), flow()))) is None
+    assert _global_batch(zip(ia, iter([(frames, frames)]))) is None
+    ic, idd = flow(), flow()
+    next(ic)
+    next(idd)
+    next(idd)
+    assert _global_batch(zip(ic, idd)) is None  # 4 vs 3: they disagree

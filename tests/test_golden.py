@@ -224,3 +224,43 @@ def test_gpu_sdr512_frames(k):
     assert psnr >= 100.0
     assert abs(p_gpu - p_ref) < 0.01
     assert np.mean(u8 != u8r) < 1e-3 and np.abs(u8.astype(int) - u8r).max() <= 1
+
+
+@pytest.mark.gpu
+def test_gpu_sdr1080_mosaic():
+    """The north star's parity at the benchmarked frame size, end to end: the 12 SDR
+    frames' centre crops tiled into ONE real-content 1080x1920 frame
+    (make_golden.mosaic1080) through U_net(input_size=(1080, 1920, 3), pad=True,
+    dtype="float32").predict on the GPU, against the fp64 oracle on the host with the
+    same zero-pad to 1088 rows and crop (predict.py:59-64, model.py:204-278).  The
+    oracle's output is pinned to the committed sdr1080.npz summary first.
+    Bounds: per-pixel max-abs <= 1e-5, PSNR(gpu, oracle) >= 100 dB, PSNR against the
+    input within 0.01 dB of the oracle's, predict.py:64 uint8 within +-1."""
+    _gpu()
+    from make_golden import mosaic1080, oracle_padded
+    import cnn_itmo_amd as C
+    z = load("sdr1080.npz")
+    names = [str(n) for n in z["names"]]
+    P = seeded_unet_params(*z["w_seed"].tolist())
+    x = R.png_to_input(mosaic1080([_png(nm) for nm in names]))[None]
+    C.clear_session()
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = C.U_net(input_size=(1080, 1920, 3), pad=True, dtype="float32", verbose=False)
+    m.set_named_weights(P)
+    y = m.predict(x).astype(np.float64)
+    C.clear_session()
+    assert y.shape == (1, 1080, 1920, 3)
+    ref = oracle_padded(P, x)
+    check_summary(z, "y", {"out": ref}, rtol=1e-9, atol=1e-12)  # oracle == fixture
+    err = float(np.abs(y - ref).max())
+    psnr = 10 * np.log10(1.0 / max(float(np.mean((y - ref) ** 2)), 1e-300))
+    p_gpu = 10 * np.log10(1 / np.mean((y - x) ** 2))
+    p_ref = 10 * np.log10(1 / np.mean((ref - x) ** 2))
+    assert abs(p_ref - float(z["psnr_vs_input"])) < 1e-9
+    u8, u8r = R.output_to_png(y[0]), R.output_to_png(ref[0])
+    print(f"1080x1920 mosaic: max-abs {err:.2e}, PSNR(gpu, oracle) {psnr:.1f} dB, |dPSNR| {abs(p_gpu - p_ref):.2e} dB, "
+          f"uint8 mismatches {int(np.sum(u8 != u8r))} of {u8.size}")
+    assert err <= 1e-5
+    assert psnr >= 100.0
+    assert abs(p_gpu - p_ref) < 0.01
+    assert np.abs(u8.astype(int) - u8r).max() <= 1

@@ -41,7 +41,8 @@ def test_dp_two_ranks_one_gpu(dtype):
     r = subprocess.run(cmd, env=_env(DTYPE=dtype), capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "ranks identical" in r.stdout
-    print(r.stdout.strip().splitlines()[-1])
+    assert r.stdout.count("Model.fit") == 2, r.stdout  # 11 frames (ragged tail) and 9 (tail dropped)
+    print("\n".join(r.stdout.strip().splitlines()[-3:]))
 
 
 def test_bench_spawns_ranks():

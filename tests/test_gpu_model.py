@@ -15,6 +15,7 @@ Tolerances (stated per north star):
   bf16 (bf16 storage, fp32 accumulation): output max-abs <= 3e-2; one step: loss
   rel <= 2e-2 and the head's gradients rel-L2 <= 0.1; functional: bf16 training
   tracks fp32 training (final loss within 10%)."""
+import os
 import io
 import contextlib
 
@@ -319,3 +320,38 @@ def test_unet_train_step_all_74_grads_128(dtype):
         assert abs(la[0] - loss) <= 5e-3 * loss
         bad = {k: (err[k], floor[k]) for k in rg if err[k] > max(3 * floor[k], 2e-3)}
     assert not bad, bad
+
+
+_HALO_OFF = r"""
+import contextlib, io, sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+import cnn_itmo_amd as C
+from cnn_itmo_amd.engine import ConcatStage
+with contextlib.redirect_stdout(io.StringIO()):
+    m = C.U_net(input_size=(64, 64, 3), dtype="bfloat16", seed=3, verbose=False)
+rng = np.random.default_rng(0)
+x = rng.uniform(size=(2, 64, 64, 3)); t = rng.uniform(size=(2, 64, 64, 3))
+la = m.train_on_batch(x, t)
+y = m.predict(x)
+split = [st.vout.split for st in m._engine().stages if isinstance(st, ConcatStage)]
+print("split", split, "loss", la[0], "finite", bool(np.isfinite(y).all()))
+"""
+
+
+@pytest.mark.parametrize("halo", ["1", "0"])
+def test_bf16_training_without_halo_kernel(halo):
+    """The split level-0 concat (Engine._plan_split_concats) is planned only where its
+    two-source forward runs: with the halo kernel disabled (CNNITMO_HALO=0, read once per
+    process) the concat stays one buffer and bf16 training and predict still work."""
+    import subprocess
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CNNITMO_HALO=halo)
+    r = subprocess.run([_sys.executable, "-c", _HALO_OFF.format(root=root)], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("split")][-1]
+    print(f"CNNITMO_HALO={halo}: {line}")
+    assert "finite True" in line
+    if halo == "0":
+        assert "True" not in line.split("loss")[0], line

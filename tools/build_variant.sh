@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a variant of libcnnitmo.so with ONE source recompiled under extra flags
-# (for tools/ab_libs.sh; CPU side, before a gpurun call):
+# (for `tools/recipe.sh layers`; CPU side, before a gpurun call):
 #   bash tools/build_variant.sh <name> <csrc file.hip | path to another version of it> -DMACRO=value ...
 # -> cnn_itmo_amd/lib/variants/lib<name>.so (git-ignored, travels with the tree)
 set -e

@@ -18,6 +18,10 @@ Checks (rank 0):
     same roundings: near-zero gradients would otherwise flip sign, and RMSprop's first
     step moves every such weight by a full +-lr*sqrt(10));
   * the epoch loss equals the sample-weighted mean of the replay's per-share losses.
+  * ``Model.fit(x, y, batch_size=B, distributed=True)`` -- batch_size is PER RANK, as
+    for the generators -- on 11 frames (global batches 4, 4, 3: shares 2+2, 2+2, 2+1)
+    and on 9 frames (4, 4, then a 1-frame tail with fewer frames than ranks, dropped on
+    every rank): the step count, identical replicas and the same single-process replay.
 
   CNNITMO_DEVICE=0 CNNITMO_DIST_BACKEND=gloo python -m torch.distributed.run \\
       --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/dp_rehearsal.py
@@ -78,44 +82,87 @@ def main():
     if rank == 0:
         assert len(set(out)) == 1, f"ranks diverged: {out}"
         # single-process replay at the global batch size
-        r = model(dtype)
-        e2 = r._engine()
         rx = ImageDataGenerator(**AUG).flow(X, batch_size=B * world, seed=1, world=1)
         ry = ImageDataGenerator(**AUG).flow(Y, batch_size=B * world, seed=1, world=1)
-        lsum, nsum = 0.0, 0
-        for s in range(STEPS):
-            xb, yb = next(rx), next(ry)
-            parts = [np.array_split(np.arange(len(xb)), world)[k] for k in range(world)]
-            acc = torch.zeros_like(e2.grads)
-            b0 = e2.bufs.clone()
-            bacc = torch.zeros_like(e2.bufs)
-            for k, ix in enumerate(parts):
-                e2.bufs.copy_(b0)
-                ix = torch.as_tensor(ix, device=xb.device)
-                if dtype == "float32":
-                    la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False)
-                    acc += e2.grads * (len(ix) / len(xb))  # the global batch mean's gradient
-                else:
-                    la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False, grad_frames=len(xb) / world)
-                    acc += e2.grads
-                lsum += float(la[0]) * len(ix)
-                nsum += len(ix)
-                bacc += e2.bufs
-            e2.step -= world - 1
-            e2.bufs.copy_(bacc * (1.0 / world))
-            ops.rmsprop(e2.params, acc, e2.accum, 1e-3, 0.9, 1e-7, 1.0 if dtype == "float32" else 1.0 / world)
-            e2.weights_dirty = True
-        torch.cuda.synchronize()
-        q = e2.params.cpu().numpy()
-        qb = e2.bufs.cpu().numpy()
+        q, qb, lmean = replay(dtype, world, [(next(rx), next(ry)) for _ in range(STEPS)])
         err = float(np.abs(p - q).max())
         berr = float(np.abs(bufs - qb).max())
-        lerr = abs(hist.history["loss"][0] - lsum / nsum)
+        lerr = abs(hist.history["loss"][0] - lmean)
         print(f"dp rehearsal: {world} ranks identical ({out[0][:12]}), max |dp - replay| params = {err:.3e}, "
-              f"moving stats = {berr:.3e}, epoch loss {hist.history['loss'][0]:.6f} vs {lsum / nsum:.6f}")
+              f"moving stats = {berr:.3e}, epoch loss {hist.history['loss'][0]:.6f} vs {lmean:.6f}")
         assert err <= 1e-6 * max(1.0, float(np.abs(q).max())), err
         assert berr <= 1e-6 * max(1.0, float(np.abs(qb).max())), berr
-        assert lerr <= 1e-6 * max(1.0, lsum / nsum), lerr
+        assert lerr <= 1e-6 * max(1.0, lmean), lerr
+    dist.barrier()
+    for nfr in (NFR, 9):
+        fit_phase(dtype, rank, world, nfr)
+
+
+def replay(dtype, world, batches):
+    """Single process: each global batch split into the ranks' shares (np.array_split),
+    each share run with that rank's dropout seed from the same state, gradients weighted
+    by the share's size, moving statistics averaged, one RMSprop step per global batch.
+    -> (params, moving stats, sample-weighted mean loss)."""
+    r = model(dtype)
+    e2 = r._engine()
+    lsum, nsum = 0.0, 0
+    for s, (xb, yb) in enumerate(batches):
+        parts = [np.array_split(np.arange(len(xb)), world)[k] for k in range(world)]
+        acc = torch.zeros_like(e2.grads)
+        b0 = e2.bufs.clone()
+        bacc = torch.zeros_like(e2.bufs)
+        for k, ix in enumerate(parts):
+            e2.bufs.copy_(b0)
+            ix = torch.as_tensor(ix, device=xb.device)
+            if dtype == "float32":
+                la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False)
+                acc += e2.grads * (len(ix) / len(xb))  # the global batch mean's gradient
+            else:
+                la = e2.train_step(xb[ix], yb[ix], seed=s * world + k, apply=False, grad_frames=len(xb) / world)
+                acc += e2.grads
+            lsum += float(la[0]) * len(ix)
+            nsum += len(ix)
+            bacc += e2.bufs
+        e2.step -= world - 1
+        e2.bufs.copy_(bacc * (1.0 / world))
+        ops.rmsprop(e2.params, acc, e2.accum, 1e-3, 0.9, 1e-7, 1.0 if dtype == "float32" else 1.0 / world)
+        e2.weights_dirty = True
+    torch.cuda.synchronize()
+    return e2.params.cpu().numpy(), e2.bufs.cpu().numpy(), lsum / nsum
+
+
+def fit_phase(dtype, rank, world, nfr):
+    """Model.fit under DP: batch_size is per rank (global batch B * world); a global
+    batch with fewer frames than ranks is dropped on every rank."""
+    X, Y = frames()
+    X = (X[:nfr] / 255.0).astype(np.float32)
+    Y = (Y[:nfr] / 255.0).astype(np.float32)
+    m = model(dtype)
+    if rank != 0:
+        m.set_named_weights({k: v + 0.25 for k, v in m.named_weights().items() if k.endswith("/kernel")})
+    hist = m.fit(X, Y, batch_size=B, epochs=1, shuffle=False, verbose=0, distributed=True)
+    gb = B * world
+    blocks = [np.arange(i, min(i + gb, nfr)) for i in range(0, nfr, gb)]
+    blocks = [b for b in blocks if len(b) >= world]
+    eng = m.engine
+    assert eng.step == len(blocks), (eng.step, len(blocks))
+    torch.cuda.synchronize()
+    p, bufs = eng.params.cpu().numpy(), eng.bufs.cpu().numpy()
+    out = [None] * world
+    dist.all_gather_object(out, hashlib.sha256(p.tobytes() + bufs.tobytes()).hexdigest())
+    if rank == 0:
+        assert len(set(out)) == 1, f"Model.fit ranks diverged: {out}"
+        dev = eng.params.device
+        q, qb, lmean = replay(dtype, world, [(torch.as_tensor(X[b], device=dev), torch.as_tensor(Y[b], device=dev))
+                                             for b in blocks])
+        err = float(np.abs(p - q).max())
+        lerr = abs(hist.history["loss"][0] - lmean)
+        print(f"Model.fit {nfr} frames: {len(blocks)} steps (global batches {[len(b) for b in blocks]}), "
+              f"ranks identical, max |dp - replay| params = {err:.3e}, epoch loss {hist.history['loss'][0]:.6f} "
+              f"vs {lmean:.6f}")
+        assert err <= 1e-6 * max(1.0, float(np.abs(q).max())), err
+        assert float(np.abs(bufs - qb).max()) <= 1e-6 * max(1.0, float(np.abs(qb).max()))
+        assert lerr <= 1e-6 * max(1.0, lmean), lerr
     dist.barrier()
 
 

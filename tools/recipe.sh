@@ -1,0 +1,79 @@
+#!/bin/bash
+# One parametrised recipe for every GPU-box measurement (run through gpurun).  Each
+# step writes under gpurun_out/; chain steps with && so the first failure ends the call.
+#
+#   bash tools/recipe.sh suite    <tag>                        full `pytest -m gpu`
+#   bash tools/recipe.sh tests    <tag> [LIB=<.so>] <pytest args...>   a subset (optionally on a variant library)
+#   bash tools/recipe.sh bench    <tag> [bench args...]        bench.py line -> <tag>_bench.json (+ .err)
+#   bash tools/recipe.sh evidence <tag>                        PMC traffic per shape, rocprofv3 stats of the
+#                                                              1080p and 4K training legs, default bench line
+#   bash tools/recipe.sh layers   <tag> <layers> <ops> <lib.so>...   per-layer A/B: in-tree library vs variants,
+#                                                              interleaved twice (tools/bench_layers.py)
+#   bash tools/recipe.sh env      <tag> "<VAR=value>" <layers> <ops>  per-layer A/B under an environment switch
+#   bash tools/recipe.sh benchab  <tag> "<VAR=value>|<lib.so>" [bench args...]   bench A/B, interleaved twice
+#   bash tools/recipe.sh pmc      <tag> <layers> <ops> "<counters>"  one rocprofv3 --pmc pass over bench_layers
+#
+# Variant libraries come from tools/build_variant.sh (CPU side, before the call).
+set -e
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+O=$R/gpurun_out
+LIB=$R/cnn_itmo_amd/lib/libcnnitmo.so
+T="timeout -k 10"
+cmd=$1; tag=$2; shift 2
+mkdir -p "$O"
+cd "$R"
+
+layers() {  # lib layers ops
+  CNNITMO_LIB=$1 $T 180 python "$R/tools/bench_layers.py" --layers "$2" --ops "$3" --iters 5 2>&1 | grep -v amdgpu.ids
+}
+
+case $cmd in
+suite)
+  $T 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/${tag}_gpu_tests.log" 2>&1
+  tail -2 "$O/${tag}_gpu_tests.log" ;;
+tests)
+  lib=$LIB
+  case $1 in LIB=*) lib=${1#LIB=}; shift ;; esac
+  CNNITMO_LIB=$lib $T 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread "$@" > "$O/${tag}_tests.log" 2>&1
+  tail -2 "$O/${tag}_tests.log" ;;
+bench)
+  $T 900 python3 bench.py "$@" > "$O/${tag}_bench.json" 2> "$O/${tag}_bench.err"
+  cat "$O/${tag}_bench.json" ;;
+evidence)
+  bash "$R/tools/pmc_traffic.sh"
+  bash "$R/tools/profile_round.sh" "$tag" --steps 5 --warmup 2 --infer-batch 0 --ns-batch 0 --k4-batch 0
+  bash "$R/tools/profile_round.sh" "${tag}_4k" --height 2160 --width 3840 --batch 8 --steps 5 --warmup 2 \
+    --infer-batch 0 --ns-batch 0 --k4-batch 0
+  cd "$R"
+  $T 900 python3 bench.py > "$O/${tag}_bench.json" 2> "$O/${tag}_bench.err"
+  cat "$O/${tag}_bench.json" ;;
+layers)
+  L=$1; P=$2; shift 2
+  for rep in 1 2; do
+    for lib in "$LIB" "$@"; do echo "== $(basename "$lib")"; layers "$lib" "$L" "$P"; done
+  done > "$O/${tag}_ab.txt" 2>&1
+  cat "$O/${tag}_ab.txt" ;;
+env)
+  sw=$1; L=$2; P=$3
+  for e in "" "$sw" "" "$sw"; do
+    echo "== ${e:-baseline}"
+    env $e CNNITMO_LIB=$LIB $T 180 python "$R/tools/bench_layers.py" --layers "$L" --ops "$P" --iters 5 2>&1 | grep -v amdgpu.ids
+  done > "$O/${tag}_ab.txt" 2>&1
+  cat "$O/${tag}_ab.txt" ;;
+benchab)
+  sw=$1; shift
+  for e in "" "$sw" "" "$sw"; do
+    case $e in *.so) envs="CNNITMO_LIB=$e" ;; "") envs="CNNITMO_LIB=$LIB" ;; *) envs=$e ;; esac
+    echo "== ${e:-baseline}"
+    env $envs $T 600 python3 bench.py --no-cpu "$@" 2>> "$O/${tag}_ab.err" | grep -E '^\{' | python3 -c \
+      "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], r['kernel'], r['achieved'])"
+  done > "$O/${tag}_ab.txt"
+  cat "$O/${tag}_ab.txt" ;;
+pmc)
+  L=$1; P=$2; ctr=$3
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d "$O/pmc_$tag" -o run -- \
+    python3 "$R/tools/bench_layers.py" --layers "$L" --ops "$P" --iters 1 > "$O/pmc_${tag}.log" 2>&1 ;;
+*)
+  echo "unknown recipe step: $cmd" >&2; exit 2 ;;
+esac
