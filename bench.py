@@ -175,9 +175,10 @@ class KernelTimer:
             fl = 2.0 * m * out.c * 27  # algorithmic K = 3x3x3 (the packed 32 has 5 zero columns)
             return self._bracket(self.fwd_name(dt, out.c), fl, "c3in fwd", o["conv1tap_fwd"], dt, cols, kk, m, wt, bias, out, *a, **k)
 
-        def conv_c3_fwd(x, n, hv, h, w, *a, **k):
+        def conv_c3_fwd(dt, x, n, hv, h, w, *a, **k):
             fl = 2.0 * n * h * w * 32 * 27
-            return self._bracket("conv_c3_fwd_kernel", fl, "c3 fwd", o["conv_c3_fwd"], x, n, hv, h, w, *a, **k)
+            return self._bracket("conv_c3_fwd_kernel" + ("<f32>" if dt == 0 else ""), fl, "c3 fwd", o["conv_c3_fwd"],
+                                 dt, x, n, hv, h, w, *a, **k)
 
         def conv_c3_wgrad(x, n, hv, h, w, *a, **k):
             fl = 2.0 * n * h * w * 32 * 27

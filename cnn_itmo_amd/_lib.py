@@ -61,7 +61,7 @@ SIGNATURES = {
     "cnnitmo_conv_c3_stat_rows": (i64, [i32, i32, i32]),
     "cnnitmo_bn_bwd_apply_g3": (i32, [i32, vp, vp, vp, i32, i32, i64, i32, vp, vp, vp, vp]),
     "cnnitmo_head_fwd_bwd_g3": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, f64, vp]),
-    "cnnitmo_conv_c3_fwd": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]),
+    "cnnitmo_conv_c3_fwd": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_conv_c3_wgrad_workspace_bytes": (sz, [i32, i32, i32]),
     "cnnitmo_conv_c3_wgrad": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, sz, vp]),
     "cnnitmo_conv1tap_fwd": (i32, [i32, vp, i32, i64, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),

@@ -25,6 +25,13 @@
 //                         slab per workgroup, fixed-order fold.
 //
 // HBM-bound: fwd 12 B read + 64 B written per pixel (+ stats), wgrad 12 + 64 B read.
+//
+// The forward also runs in fp32 (TO = float, the fp32 inference path of predict.py:62):
+// the same per-lane operand (8 k-values gathered from the fp32 image) goes to the MFMA
+// as two 16-byte fp32 fragments (Mma<float>: four 16x16x4 f32 MFMAs each) against the
+// weights in the same k order, and each (pixel, 8 channels) leaves as two 16-byte
+// stores: 12 B read + 128 B written per pixel, replacing im2col (128 B written, 128 B
+// read back) + a 1-tap GEMM.
 #include "dma.h"
 #include "igemm_common.h"
 
@@ -55,9 +62,9 @@ struct C3Fwd2 {
   const float* x;
   int n, hv, h, w, segs, rpn;
   long units;
-  const bf16* wt;  // [32 cout][32 k]
+  const void* wt;  // [32 cout][32 k] in TO
   const float* bias;
-  bf16* out;
+  void* out;
   long out_ld;
   int out_off;
   int flags;
@@ -69,8 +76,9 @@ struct C3Fwd2 {
 #ifndef C3_MINW
 #define C3_MINW 3                           // waves per SIMD the register budget is sized for
 #endif
-template <bool AFF>
+template <typename TO, bool AFF>
 __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 a) {
+  constexpr bool F32 = sizeof(TO) == 4;
   __shared__ __attribute__((aligned(1024))) float xs[2][XBUF];
   __shared__ float red[4][2][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -87,14 +95,23 @@ __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 
   for (int e = 0; e < 8; ++e) koff[e] = g < 3 ? e : (e < 3 ? e * XRW : 0);
   // weights (A operand: row i of block j = output channel pair_perm(16j + i), its
   // k' values gathered from the [32 cout][32 k] (k = tap*3 + c) rows)
-  uint4 bw[2];
+  // (fp32: the 8 values as two 16-byte fragments, k order e = 4h + i in both operands)
+  uint4 bw[2][F32 ? 2 : 1];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const bf16* wr = a.wt + pair_perm(16 * j + pxl) * 32;
-    bf16x8 t;
+    const TO* wr = (const TO*)a.wt + pair_perm(16 * j + pxl) * 32;
+    float t[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) t[e] = g < 3 ? wr[9 * g + e] : (e < 3 ? wr[9 * e + 8] : (bf16)0.f);
-    bw[j] = __builtin_bit_cast(uint4, t);
+    for (int e = 0; e < 8; ++e) t[e] = g < 3 ? to_f32(wr[9 * g + e]) : (e < 3 ? to_f32(wr[9 * e + 8]) : 0.f);
+    if constexpr (F32) {
+      bw[j][0] = __builtin_bit_cast(uint4, f32x4{t[0], t[1], t[2], t[3]});
+      bw[j][1] = __builtin_bit_cast(uint4, f32x4{t[4], t[5], t[6], t[7]});
+    } else {
+      bf16x8 tb;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) tb[e] = (bf16)t[e];
+      bw[j][0] = __builtin_bit_cast(uint4, tb);
+    }
   }
   const bool relu = a.flags & CNNITMO_RELU, stats = a.flags & CNNITMO_STATS;
   float bj[8], sj[AFF ? 8 : 1], hj[AFF ? 8 : 1], s1[8], s2[8];
@@ -165,15 +182,29 @@ __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 
         const float* src = X + rr * XRW + kb + (p0 + pxl + 3) * 3;
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          bf16x8 xb;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xb[e] = from_f32<bf16>(src[f * 48 + koff[e]]);
-          const uint4 xf = __builtin_bit_cast(uint4, xb);
           f32x4 acc[2];
+          if constexpr (F32) {
+            float xv[8];
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            Mma<bf16>::run(acc[j], bw[j], xf);  // C^T: lanes = pixels
+            for (int e = 0; e < 8; ++e) xv[e] = src[f * 48 + koff[e]];
+            const uint4 x0 = __builtin_bit_cast(uint4, f32x4{xv[0], xv[1], xv[2], xv[3]});
+            const uint4 x1 = __builtin_bit_cast(uint4, f32x4{xv[4], xv[5], xv[6], xv[7]});
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+              Mma<float>::run(acc[j], bw[j][0], x0);  // C^T: lanes = pixels
+              Mma<float>::run(acc[j], bw[j][F32 ? 1 : 0], x1);
+            }
+          } else {
+            bf16x8 xb;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xb[e] = from_f32<bf16>(src[f * 48 + koff[e]]);
+            const uint4 xf = __builtin_bit_cast(uint4, xb);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+              Mma<bf16>::run(acc[j], bw[j][0], xf);  // C^T: lanes = pixels
+            }
           }
           const int px = p0 + f * 16 + pxl;
           const bool ok = px < npx;
@@ -188,7 +219,11 @@ __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 
             s1[k] += vs;
             s2[k] += vs * vs;
           }
-          if (ok) Pack16<bf16>::store(a.out + (prow + px) * a.out_ld + a.out_off + 8 * g, v);
+          if (ok) {
+            TO* o = (TO*)a.out + (prow + px) * a.out_ld + a.out_off + 8 * g;
+            Pack16<TO>::store(o, v);
+            if constexpr (F32) Pack16<TO>::store(o + 4, v + 4);
+          }
         }
       }
     }
@@ -380,12 +415,14 @@ extern "C" long cnnitmo_conv_c3_stat_rows(int n, int h, int w) {
   return std::min<long>(c3_units(n, h, w), C3_GRID);
 }
 
-extern "C" int cnnitmo_conv_c3_fwd(const float* x, int n, int h_valid, int h, int w, const void* wt,
+extern "C" int cnnitmo_conv_c3_fwd(int dtype, const float* x, int n, int h_valid, int h, int w, const void* wt,
                                    const float* bias, void* out, int out_ld, int out_off, int flags,
                                    const float* aff_scale, const float* aff_shift, float* stat_part, void* stream) {
+  CNN_REQUIRE(dtype == CNNITMO_BF16 || dtype == CNNITMO_F32, "conv_c3_fwd: unsupported dtype %d", dtype);
   CNN_REQUIRE(x && wt && out, "conv_c3_fwd: null pointer");
   CNN_REQUIRE(n > 0 && h > 0 && w > 0 && h_valid >= 0 && h_valid <= h, "conv_c3_fwd: bad shape");
-  CNN_REQUIRE(out_ld % 8 == 0 && out_off % 8 == 0 && out_ld >= out_off + 32, "conv_c3_fwd: output view");
+  const int al = dtype == CNNITMO_BF16 ? 8 : 4;  // 16-byte aligned pixel rows
+  CNN_REQUIRE(out_ld % al == 0 && out_off % al == 0 && out_ld >= out_off + 32, "conv_c3_fwd: output view");
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || stat_part, "conv_c3_fwd: STATS without buffer");
   CNN_REQUIRE(!(flags & CNNITMO_AFFINE) || (aff_scale && aff_shift), "conv_c3_fwd: AFFINE without coefficients");
   C3Fwd2 a;
@@ -393,14 +430,20 @@ extern "C" int cnnitmo_conv_c3_fwd(const float* x, int n, int h_valid, int h, in
   a.segs = (w + SEG - 1) / SEG;
   a.rpn = (h + RPB - 1) / RPB;
   a.units = c3_units(n, h, w);
-  a.wt = (const bf16*)wt; a.bias = bias; a.out = (bf16*)out; a.out_ld = out_ld; a.out_off = out_off;
+  a.wt = wt; a.bias = bias; a.out = out; a.out_ld = out_ld; a.out_off = out_off;
   a.flags = flags; a.aff_scale = aff_scale; a.aff_shift = aff_shift; a.stats = stat_part;
   CNN_REQUIRE((long)h_valid * w * 3 < (1L << 29), "conv_c3_fwd: frame too large for 32-bit offsets");
   const long blocks = cnnitmo_conv_c3_stat_rows(n, h, w);
-  if (flags & CNNITMO_AFFINE)
-    hipLaunchKernelGGL(conv_c3_fwd_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(conv_c3_fwd_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a);
+  const dim3 grid((unsigned)blocks);
+  hipStream_t s = (hipStream_t)stream;
+  const bool af = flags & CNNITMO_AFFINE;
+  if (dtype == CNNITMO_F32) {
+    if (af) hipLaunchKernelGGL((conv_c3_fwd_kernel<float, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_c3_fwd_kernel<float, false>), grid, dim3(256), 0, s, a);
+  } else {
+    if (af) hipLaunchKernelGGL((conv_c3_fwd_kernel<bf16, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((conv_c3_fwd_kernel<bf16, false>), grid, dim3(256), 0, s, a);
+  }
   return cnnitmo_check_launch("conv_c3_fwd");
 }
 

@@ -119,7 +119,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   constexpr int FN = C::FN, FP = C::FP, L = C::L, NBI = C::NBI, STAGE = C::STAGE, ST = C::ST;
   constexpr int ES = sizeof(TE), CC = 64 / ES, PE = 16 / ES;
   constexpr int NST = C::NST * (ES == 4 ? 2 : 1);  // stores per wave per epilogue
-  static_assert(ES == 2 || EPI == 1, "fp32: the forward epilogue only");
+  static_assert(ES == 2 || EPI != 2, "fp32: forward and plain input-gradient epilogues");
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -629,7 +629,8 @@ int halo_ncu() {
 }
 
 // conv3x3 stride 1 'same' (forward or input-gradient), 64-byte chunks (32 bf16 / 16 fp32
-// channels); fp32: the inference forward only (EPI 1 without BN sums, one source)
+// channels); fp32: the forward (EPI 1, with BN sums for training) and the plain input
+// gradient (EPI 0), one source
 bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_HALO");
@@ -644,8 +645,7 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   if (!en || (f32 && !en32)) return false;
   if (f32) {
     if (a.cin % 16 || a.a_ld % 4 || a.a_off % 4 || a.out_ld % 4 || a.out_off % 4) return false;
-    if (a.a2 || a.bnb_out || a.stats || (a.flags & CNNITMO_STATS)) return false;
-    if (!(a.flags || a.bias || a.border)) return false;  // EPI 1
+    if (a.a2 || a.bnb_out) return false;
   } else if (a.cin % 32 || a.a_ld % 8 || a.a_off % 8 || a.out_ld % 8 || a.out_off % 8) {
     return false;
   }
@@ -701,9 +701,12 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
   CNN_REQUIRE(h.tiles * h.nchunks < (1L << 31), "%s: too many tiles", what);
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
   const int grid = halo_ncu();
-  if (f32) {
+  if (f32 && pl.epi == 1) {
     if (pl.bn == 64) launch_cfg<float, 64, 1>(h, pl.res, grid, s);
     else launch_cfg<float, 32, 1>(h, pl.res, grid, s);
+  } else if (f32) {
+    if (pl.bn == 64) launch_cfg<float, 64, 0>(h, pl.res, grid, s);
+    else launch_cfg<float, 32, 0>(h, pl.res, grid, s);
   } else if (pl.epi == 2) {
     if (pl.bn == 64) launch_cfg<bf16, 64, 2>(h, pl.res, grid, s);
     else launch_cfg<bf16, 32, 2>(h, pl.res, grid, s);
@@ -726,8 +729,8 @@ const char* halo_name(const FwdArgs& a, bool f32) {
 }
 
 // BN partial-sum rows written by the halo kernel: one per (stream, wave).
-long halo_stat_rows(const FwdArgs& a) {
+long halo_stat_rows(const FwdArgs& a, bool f32) {
   HaloPlan pl;
-  if (!halo_plan(a, pl)) return 0;
+  if (!halo_plan(a, pl, f32)) return 0;
   return (long)halo_streams(a, pl) * NWAVE;
 }

@@ -115,10 +115,10 @@ int fwd2_bm(const FwdArgs& a, bool bf16);  // row tile of the v2 launch (128 or 
 bool fwd2_t256(const FwdArgs& a, bool bf16);  // 256 x 256 tiles (bf16 tconv input gradient)
 
 // halo-tiled 3x3 conv (bf16, 4x64 output tiles), conv_halo.hip
-bool halo_handles(const FwdArgs& a, bool f32 = false);  // f32: the fp32 inference forward
+bool halo_handles(const FwdArgs& a, bool f32 = false);  // f32: the fp32 forward / plain dgrad
 int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32 = false);
 const char* halo_name(const FwdArgs& a, bool f32 = false);
-long halo_stat_rows(const FwdArgs& a);
+long halo_stat_rows(const FwdArgs& a, bool f32 = false);
 
 // tconv_stream.hip: Conv2DTranspose fwd (mode 0) / input-gradient (mode 1) as a
 // streamed GEMM with the weight block resident in LDS (bf16)

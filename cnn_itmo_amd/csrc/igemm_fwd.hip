@@ -334,6 +334,7 @@ extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int ci
   set_taps3x3(a);
   a.cin = cin; a.N = cout; a.a_ld = cin; a.out_ld = cout; a.M = (long)n * h * w;
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_stat_rows(a);
+  if (dtype == CNNITMO_F32 && halo_handles(a, true)) return halo_stat_rows(a, true);
   return cnnitmo_fwd_stat_rows(dtype, a.M, cout);
 }
 

@@ -335,11 +335,10 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
   }();
   if (!en || cout % 32 || cin % 32) return false;
   const int K = mode == 0 ? cin : 4 * cout, N = mode == 0 ? 4 * cout : cin;
-  // K = 256 or 512: the row padding below is conflict-free (K % 128 == 0) and the K loop
-  // is compiled for K / 32 = 8 or 16 steps (a multiple of TWS_PD)
-  if (K != 256 && K != 512) return false;
-  if (f32) {  // fp32 inference forward: the widest block whose fp32 rows fit (K 512: 64, 256: 128)
-    if (!en32 || mode != 0) return false;
+  if (f32) {  // fp32 inference forward: the widest block whose fp32 rows fit (K 512: 64, 256 / 128: 128)
+    // K = 128 is up9 (128 -> 64 channels at full resolution), which ran on igemm_fwd2's
+    // 128 x 128 tiles at 0.49 of fp32 peak (a 256-column block spills: 16 fp32 fragments)
+    if (!en32 || mode != 0 || (K != 128 && K != 256 && K != 512)) return false;
     const int bn = K == 512 ? 64 : 128;
     if (N % bn || N / bn > 32 || 32 % (N / bn)) return false;
     pl.bn = bn;
@@ -347,6 +346,9 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
     pl.gpx = 32 / pl.nblk;
     return true;
   }
+  // K = 256 or 512: the row padding below is conflict-free (K % 128 == 0) and the K loop
+  // is compiled for K / 32 = 8 or 16 steps (a multiple of TWS_PD)
+  if (K != 256 && K != 512) return false;
   static const int bn256 = [] {
     const char* e = getenv("CNNITMO_TWS_BN256");
     return e ? atoi(e) : 0;
@@ -431,13 +433,15 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 256, 8, 1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 64, 32, 2, 2, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
 #define TWL(M, KS) hipLaunchKernelGGL((tconv_ws_kernel<M, 128, KS>), dim3(grid), dim3(NW * 64), lds, s, t)
   if (f32) {  // K / 16 steps
     if (t.K == 512) hipLaunchKernelGGL((tconv_ws_kernel<0, 64, 32, 2, 2, float>), dim3(grid), dim3(NW * 64), lds, s, t);
-    else hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 16, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
+    else if (t.K == 256) hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 16, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
+    else hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 8, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
   } else if (pl.bn == 256) {
     hipLaunchKernelGGL((tconv_ws_kernel<0, 256, 8, 1, 4>), dim3(grid), dim3(NW * 64), lds, s, t);
   } else if (mode == 0) {

@@ -173,9 +173,11 @@ class BlockStage(Stage):
             self.w_fwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
             self.w_bwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
         self.foldable = self.kind != "c3in" and self.vin.folded
-        # first layer without im2col (bf16, 32 filters; CNNITMO_C3_DIRECT=0: im2col + 1-tap GEMM)
-        self.direct = (self.kind == "c3in" and eng.dt == L.BF16 and cout == 32
-                       and os.environ.get("CNNITMO_C3_DIRECT", "1") != "0")
+        # first layer without im2col (32 filters; CNNITMO_C3_DIRECT=0: im2col + 1-tap GEMM):
+        # bf16 always (conv_c3 forward and weight gradient); fp32 for inference forwards
+        # (the fp32 weight gradient still reads im2col columns, so fp32 training packs them)
+        self.direct_ok = (self.kind == "c3in" and cout == 32 and os.environ.get("CNNITMO_C3_DIRECT", "1") != "0")
+        self.direct = self.direct_ok and eng.dt == L.BF16
         if self.foldable:  # per-step folded copies (training)
             f32 = torch.float32
             self.w_fold = torch.empty_like(self.w_fwd)
@@ -223,7 +225,7 @@ class BlockStage(Stage):
         elif self.kind == "c3":
             ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
         elif self.kind == "c3in" and self.direct:
-            ops.conv_c3_fwd(e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.w_fwd, bias, out_view, flags,
+            ops.conv_c3_fwd(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.w_fwd, bias, out_view, flags,
                             aff, stats)
         elif self.kind == "c3in":
             ops.conv1tap_fwd(e.dt, self.cols, 32, n * self.vout.h * self.vout.w, self.w_fwd, bias,
@@ -252,6 +254,7 @@ class BlockStage(Stage):
         cout = self.cout
         P = n * self.vout.h * self.vout.w
         self.fold_active = training and self.foldable
+        self.direct = self.direct_ok and (e.dt == L.BF16 or not training)
         if self.kind == "c3in" and not self.direct:
             self.cols = torch.empty(P * 32, dtype=e.tdtype, device=e.device)
             ops.im2col_c3(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.cols)

@@ -154,10 +154,11 @@ def conv_c3_stat_rows(n, h, w):
     return query("cnnitmo_conv_c3_stat_rows", n, h, w)
 
 
-def conv_c3_fwd(x, n, h_valid, h, w, wt, bias, out: View, flags=0, aff=None, stats=None):
-    """First layer, bf16, patches built in LDS from the fp32 input (no im2col buffer)."""
+def conv_c3_fwd(dt, x, n, h_valid, h, w, wt, bias, out: View, flags=0, aff=None, stats=None):
+    """First layer (bf16 or fp32 output), operands built from the fp32 input image (no
+    im2col buffer)."""
     sc, sh = aff if aff is not None else (None, None)
-    call("cnnitmo_conv_c3_fwd", ptr(x), n, h_valid, h, w, ptr(wt), ptr(bias), out.ptr, out.ld, out.off, flags,
+    call("cnnitmo_conv_c3_fwd", dt, ptr(x), n, h_valid, h, w, ptr(wt), ptr(bias), out.ptr, out.ld, out.off, flags,
          ptr(sc), ptr(sh), ptr(stats), stream_ptr())
 
 

@@ -176,13 +176,13 @@ int cnnitmo_conv1tap_fwd(int dtype, const void* cols, int k, long m, const void*
                          int flags, const float* aff_scale, const float* aff_shift,
                          float* stat_part, void* stream);
 
-/* First layer without im2col (bf16): x [n,h_valid,w,3] fp32 -> out view [n,h,w,32]
- * (ld, off), rows >= h_valid of the input read as zero (pad-to-16).  wt: [32][32]
- * bf16 packed columns (cnnitmo_prep_c3_weights); flags/aff as conv3x3_fwd;
+/* First layer without im2col: x [n,h_valid,w,3] fp32 -> out view [n,h,w,32] in dtype
+ * (bf16 or fp32; ld, off), rows >= h_valid of the input read as zero (pad-to-16).  wt:
+ * [32][32] packed columns in dtype (cnnitmo_prep_c3_weights); flags/aff as conv3x3_fwd;
  * stat_part [rows][2][32] with rows = cnnitmo_conv_c3_stat_rows.  Replaces
  * cnnitmo_im2col_c3 + cnnitmo_conv1tap_fwd for model.py:208. */
 long cnnitmo_conv_c3_stat_rows(int n, int h, int w);
-int cnnitmo_conv_c3_fwd(const float* x, int n, int h_valid, int h, int w, const void* wt,
+int cnnitmo_conv_c3_fwd(int dtype, const float* x, int n, int h_valid, int h, int w, const void* wt,
                         const float* bias, void* out, int out_ld, int out_off, int flags,
                         const float* aff_scale, const float* aff_shift, float* stat_part, void* stream);
 /* dw [32][27] fp32 (OVERWRITTEN; OHWI) = sum_p dz[p][co] * patch(x, p)[k], dz [n*h*w][32]

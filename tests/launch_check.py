@@ -334,16 +334,19 @@ class LaunchChecker(ElementwiseChecks):
             xp = xp.to(BF)
         return torch.nn.functional.pad(xp.to(F64), (0, 0, 0, 0, 0, h - hv))
 
-    def _chk_conv_c3_fwd(self, x, n, hv, h, w, wt, bias, out, flags=0, aff=None, stats=None):
-        xin = self._c3_input(x, n, hv, h, w, L.BF16)
+    def _chk_conv_c3_fwd(self, dt, x, n, hv, h, w, wt, bias, out, flags=0, aff=None, stats=None):
+        xin = self._c3_input(x, n, hv, h, w, dt)
         W = wt.view(32, 32)[:, :27].reshape(32, 3, 3, 3)
         lab = f"conv_c3_fwd {n}x{h}x{w} (valid {hv})"
-        acc, ot = _Acc(self, lab), out.tensor()
+        acc, ot = _Acc(self, lab, dt), out.tensor()
         s1 = torch.zeros(32, dtype=F64, device=x.device)
         sa = torch.zeros_like(s1)
         for i in range(n):
             z = _epilogue(_conv3(xin[i], W) + bias.to(F64), flags, aff)
-            acc.add(ot[i], z)
+            sl = _f32_slack(dt, 27, _conv3(xin[i].abs(), W.abs()))
+            if sl is not None and flags & L.AFFINE:
+                sl = sl * aff[0].to(F64).abs()
+            acc.add(ot[i], z, sl)
             s1 += z.sum((0, 1))
             sa += z.abs().sum((0, 1))
         acc.done()

@@ -77,7 +77,7 @@ TRAIN = ["conv_c3_fwd", "conv3x3_fwd", "conv3x3_fwd_cat", "conv_wgrad_cat", "tco
          "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3", "bn_consumer_sums", "colsum",
          "border_sums", "head_fwd_bwd_g3", "head_finalize", "rmsprop", "prep_conv3x3", "prep_tconv", "prep_c3",
          "fold_conv3x3", "fold_tconv"]
-INFER_F32 = ["prep_conv3x3", "prep_tconv", "prep_c3", "im2col_c3", "conv1tap_fwd", "conv3x3_fwd", "tconv_fwd",
+INFER_F32 = ["prep_conv3x3", "prep_tconv", "prep_c3", "conv_c3_fwd", "conv3x3_fwd", "tconv_fwd",
              "maxpool_fwd", "bn_infer_coeffs", "head_fwd"]
 
 

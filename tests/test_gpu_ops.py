@@ -230,34 +230,38 @@ def test_first_layer_im2col(dt):
     close(host(dw).reshape(dw_ref.shape), dw_ref, dt, "first layer wgrad")
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
 @pytest.mark.parametrize("N,Hv,H,W,ld,off", [(2, 13, 16, 10, 32, 0), (1, 6, 7, 300, 96, 64), (3, 9, 9, 256, 32, 0),
                                              (2, 5, 6, 517, 32, 0)])
-def test_first_layer_direct(N, Hv, H, W, ld, off):
-    """cnnitmo_conv_c3_fwd / _wgrad (bf16, no im2col buffer) vs the oracle: ReLU + BN
-    partial sums + output view, partial 256-pixel segments, zero rows >= Hv, and a
-    row count that is not a multiple of the 4-row workgroup."""
+def test_first_layer_direct(N, Hv, H, W, ld, off, dt):
+    """cnnitmo_conv_c3_fwd (bf16 and fp32 outputs) / _wgrad (bf16), no im2col buffer, vs
+    the oracle: ReLU + BN partial sums + output view, partial 256-pixel segments, zero
+    rows >= Hv, odd widths (the edge piece of every row) and a row count that is not a
+    multiple of the 4-row workgroup."""
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(19)
     x = rng.uniform(size=(N, Hv, W, 3)).astype(np.float32)
     w = (rng.standard_normal((32, 3, 3, 3)) * 0.3).astype(np.float32)
     b = rng.standard_normal(32).astype(np.float32)
-    wp = torch.empty(32 * 32, dtype=torch.bfloat16, device="cuda")
-    ops.prep_c3(DT["bf16"], torch.tensor(w).cuda(), 32, wp)
-    buf = torch.zeros(N * H * W * ld, dtype=torch.bfloat16, device="cuda")
+    wp = torch.empty(32 * 32, dtype=TDT[dt], device="cuda")
+    ops.prep_c3(DT[dt], torch.tensor(w).cuda(), 32, wp)
+    buf = torch.zeros(N * H * W * ld, dtype=TDT[dt], device="cuda")
     out = ops.View(buf, N, H, W, 32, ld, off)
     rows = ops.conv_c3_stat_rows(N, H, W)
     stats = torch.empty(rows * 64, device="cuda")
     xd = torch.tensor(x).cuda()
-    ops.conv_c3_fwd(xd, N, Hv, H, W, wp, torch.tensor(b).cuda(), out, flags=1 | 2, stats=stats)
+    ops.conv_c3_fwd(DT[dt], xd, N, Hv, H, W, wp, torch.tensor(b).cuda(), out, flags=1 | 2, stats=stats)
     xp = np.zeros((N, H, W, 3))
-    xp[:, :Hv] = rnd(x, "bf16")
-    ref = np.maximum(R.conv2d_same(xp, rnd(w, "bf16"), b), 0)
+    xp[:, :Hv] = rnd(x, dt)
+    ref = np.maximum(R.conv2d_same(xp, rnd(w, dt), b), 0)
     torch.cuda.synchronize()
     got = host(buf).reshape(N, H, W, ld)[..., off:off + 32]
-    close(got, ref, "bf16", "first layer direct")
+    close(got, ref, dt, "first layer direct")
     st = stats.cpu().numpy().reshape(rows, 2, 32).sum(0)
     np.testing.assert_allclose(st[0], ref.reshape(-1, 32).sum(0), rtol=2e-2, atol=2e-2 * ref.size / 32)
     np.testing.assert_allclose(st[1], (ref ** 2).reshape(-1, 32).sum(0), rtol=3e-2)
+    if dt == "f32":
+        return
     dz = rng.standard_normal((N, H, W, 32)).astype(np.float32)
     _, dw_ref, _ = R.conv2d_same_bwd(xp, rnd(w, "bf16"), rnd(dz, "bf16"), need_dx=False)
     dw = torch.empty(32, 27, device="cuda")
