@@ -19,8 +19,10 @@ runs on (its ms/step is reported beside).  `allreduce_exposed` (N>1) is the time
 the compute stream waits for the RCCL buckets after backward.  `cpu_baseline`
 times this repo's numpy oracle (oracle/unet_ref.py) on the host (rank 0, N=1).
 `fp32_infer` is BASELINE configs[1] (1080p b8 fp32 inference) with its own
-roofline and CPU baseline; `k4_train` is configs[4] (3840x2160, bf16 training,
-8 frames per GPU = global 64 on 8 GPUs).
+roofline and CPU baseline; `fp32_infer_b32` the north star's fp32 conv2d forward at
+1080p batch 32; `k4_train` is configs[4] (3840x2160, bf16 training, 8 frames per
+GPU = global 64 on 8 GPUs); `fp32_train` the reference's own precision (Keras fp32
+training, 1080p, 8 frames per GPU).  Each secondary leg carries its own roofline.
 """
 from __future__ import annotations
 
@@ -62,6 +64,9 @@ def parse():
                     help="4K bf16 training leg (configs[4]: 3840x2160, global 64 on 8 GPUs) frames per GPU; 0 = skip")
     ap.add_argument("--k4-steps", type=int, default=10)
     ap.add_argument("--k4-warmup", type=int, default=3)
+    ap.add_argument("--f32-train-batch", type=int, default=8,
+                    help="fp32 1080p training leg (the reference's Keras precision) frames per GPU; 0 = skip")
+    ap.add_argument("--f32-train-steps", type=int, default=5)
     ap.add_argument("--ns-batch", type=int, default=32,
                     help="north-star leg: fp32 1080p inference (conv2d forward) at this batch per GPU; 0 = skip")
     return ap.parse_args()
@@ -548,8 +553,9 @@ def main():
                 pass
 
     # configs[1]: fp32 inference leg (b8 1080p, BN moving stats), same ranks, weak
-    infer = ns = k4 = None
-    if args.mode == "train" and (args.infer_batch > 0 or args.k4_batch > 0 or args.ns_batch > 0):
+    infer = ns = k4 = f32t = None
+    if args.mode == "train" and (args.infer_batch > 0 or args.k4_batch > 0 or args.ns_batch > 0
+                                 or args.f32_train_batch > 0):
         del eng, model, x, t, losses
         timer.rec = []
         C.clear_session()
@@ -561,7 +567,10 @@ def main():
         ns = guarded(infer_leg, args, rank, world, timer, barrier, agree, P_init, H, W, args.ns_batch, False)
     # configs[4]: 4K training (b8 per GPU = global 64 on 8 GPUs), DP when N > 1
     if args.mode == "train" and args.k4_batch > 0:
-        k4 = guarded(k4_leg, args, rank, world, timer, barrier, agree, cpu if args.mode == "train" else None)
+        k4 = guarded(k4_leg, args, rank, world, timer, barrier, agree, cpu)
+    # fp32 training (the reference's precision; the drop-in default dtype of U_net)
+    if args.mode == "train" and args.f32_train_batch > 0:
+        f32t = guarded(f32_train_leg, args, rank, world, timer, barrier, agree, cpu)
 
     if rank == 0:
         res = "1080p" if (args.height, args.width) == (1080, 1920) else f"{args.width}x{args.height}"
@@ -586,6 +595,8 @@ def main():
             line["fp32_infer_b32"] = ns
         if k4 is not None:
             line["k4_train"] = k4
+        if f32t is not None:
+            line["fp32_train"] = f32t
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
@@ -680,24 +691,19 @@ def _shape(mode, h, w, b, dtype):
     return f"{mode} {h}x{w} b{b} {dtype}"
 
 
-def k4_leg(args, rank, world, timer, barrier, agree, cpu_1080):
-    """BASELINE configs[4]: 3840x2160 frames, bf16, fwd+bwd+RMSprop, k4_batch frames per
-    GPU (8 = global 64 on 8 GPUs), DP over the same ranks when N > 1.  The activations
-    are not tiled: at 8 frames per GPU the step's working set fits one GPU's HBM
-    (peak_mem_gib), so the frame is processed whole, which keeps every pixel's
-    receptive field exact.  Same two passes as the headline: K timed
-    steps without instrumentation, then min(K, 10) steps with every conv launch
-    bracketed by HIP events (roofline of the dominant kernel, PMC traffic of the
-    profiled 4K shape).  cpu_baseline: the headline leg's oracle training step (one
-    960x544 crop, same run) scaled to a 3840x2160 frame by pixel count."""
+def train_leg(args, rank, world, timer, barrier, agree, cpu_1080, Hk, Wk, B, dtype, steps, warmup, label):
+    """A secondary training leg (fwd+bwd+RMSprop, DP over the same ranks when N > 1) with
+    the headline's two passes: K timed steps without instrumentation, then min(K, 10)
+    steps with every conv launch bracketed by HIP events (roofline of the dominant
+    kernel, PMC traffic when the profiled shape matches).  cpu_baseline: the headline
+    leg's oracle training step (one 960x544 crop, same run; the oracle computes in fp32)
+    scaled to this frame size by pixel count."""
     import torch
     import cnn_itmo_amd as C
-    Hk, Wk = 2160, 3840
-    B = args.k4_batch
     ok = False
     try:  # everything that can fail alone (allocation) happens before the first collective
         with contextlib.redirect_stdout(io.StringIO()):
-            m = C.U_net(input_size=(Hk, Wk, 3), pad=True, dtype="bfloat16", seed=0, verbose=False)
+            m = C.U_net(input_size=(Hk, Wk, 3), pad=True, dtype=dtype, seed=0, verbose=False)
         eng = m._engine()
         g = torch.Generator(device="cuda")
         g.manual_seed(4321 + 7919 * rank)
@@ -730,9 +736,9 @@ def k4_leg(args, rank, world, timer, barrier, agree, cpu_1080):
             torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
         return el.item(), out
 
-    for i in range(max(1, args.k4_warmup)):
+    for i in range(max(1, warmup)):
         step(i)
-    k = max(1, args.k4_steps)
+    k = max(1, steps)
     elapsed, out = timed(k, 100)
     loss = out.cpu().numpy().tolist() if out is not None else None
     timer.reset()
@@ -742,29 +748,46 @@ def k4_leg(args, rank, world, timer, barrier, agree, cpu_1080):
     timer.on = False
     agg = timer.summary()
     Hp = -(-Hk // 16) * 16
-    roof, step_flops = _roofline(agg, k2, elapsed2, BF16_PEAK_TF, _shape("train", Hk, Wk, B, "bfloat16"))
+    peak = BF16_PEAK_TF if dtype == "bfloat16" else F32_PEAK_TF
+    roof, step_flops = _roofline(agg, k2, elapsed2, peak, _shape("train", Hk, Wk, B, dtype))
     roof["timed_pass_ms_per_step"] = round(elapsed2 / k2 * 1e3, 2)
     if rank == 0:
-        _print_agg(agg, "k4")
-        _print_detail(timer.detail(), k2, "k4")
-    res = {"metric": "4K SDR->HDR frames/sec (fwd+bwd)", "value": round(B * world * k / elapsed, 3),
-           "unit": "frames/s", "dtype": "bf16", "steps": k, "warmup": max(1, args.k4_warmup),
+        _print_agg(agg, label)
+        _print_detail(timer.detail(), k2, label)
+    res_name = "4K" if (Hk, Wk) == (2160, 3840) else ("1080p" if (Hk, Wk) == (1080, 1920) else f"{Wk}x{Hk}")
+    res = {"metric": f"{res_name} SDR->HDR frames/sec (fwd+bwd)", "value": round(B * world * k / elapsed, 3),
+           "unit": "frames/s", "dtype": "bf16" if dtype == "bfloat16" else "f32", "steps": k, "warmup": max(1, warmup),
            "ms_per_step": round(elapsed / k * 1e3, 2),
            "peak_mem_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1), "last_loss_acc": loss,
-           "config": {"workload": f"U-Net train step, {Wk}x{Hk} frames padded to {Wk}x{Hp}, {B} frames/GPU "
-                                  f"(BASELINE configs[4]; whole frames, no spatial tiling needed)",
+           "config": {"workload": f"U-Net train step, {Wk}x{Hk} frames padded to {Wk}x{Hp}, {B} frames/GPU ({label})",
                       "global_batch": B * world, "parallelism": f"dp{world}",
                       "gflop_per_frame": round(step_flops / B / 1e9, 1)},
            "roofline": roof, "cpu_baseline": None}
     if cpu_1080 and "value" in cpu_1080:
-        sc = (1920.0 * cpu_1080["padded_h"]) / (Wk * Hp)  # 1080p-frame equivalents -> 4K frames
-        res["cpu_baseline"] = {"value": cpu_1080["value"] * sc, "unit": "4K frames/s (fwd+bwd, fp32)",
+        sc = (1920.0 * cpu_1080["padded_h"]) / (Wk * Hp)  # 1080p-frame equivalents -> these frames
+        res["cpu_baseline"] = {"value": cpu_1080["value"] * sc, "unit": f"{res_name} frames/s (fwd+bwd, fp32)",
                                "cores": cpu_1080["cores"], "kind": cpu_1080["kind"],
                                "sample": cpu_1080["sample"] + f"; the same timing scaled to a {Wk}x{Hp} frame "
                                                               f"by pixel count (x{sc:.4f})",
                                "seconds": cpu_1080["seconds"], "threads_note": cpu_1080.get("threads_note")}
     del eng, m, x, t
     return res
+
+
+def k4_leg(args, rank, world, timer, barrier, agree, cpu_1080):
+    """BASELINE configs[4]: 3840x2160 frames, bf16, fwd+bwd+RMSprop, k4_batch frames per
+    GPU (8 = global 64 on 8 GPUs).  The activations are not tiled: at 8 frames per GPU
+    the step's working set fits one GPU's HBM (peak_mem_gib), so the frame is processed
+    whole, which keeps every pixel's receptive field exact."""
+    return train_leg(args, rank, world, timer, barrier, agree, cpu_1080, 2160, 3840, args.k4_batch, "bfloat16",
+                     args.k4_steps, args.k4_warmup, "BASELINE configs[4]; whole frames, no spatial tiling needed")
+
+
+def f32_train_leg(args, rank, world, timer, barrier, agree, cpu_1080):
+    """The reference's own training precision (Keras fp32, main.py:126-132) at 1080p:
+    fp32 storage and fp32 MFMA (16x16x4 f32), f32_train_batch frames per GPU."""
+    return train_leg(args, rank, world, timer, barrier, agree, cpu_1080, args.height, args.width,
+                     args.f32_train_batch, "float32", args.f32_train_steps, 2, "fp32 training, main.py:126-132")
 
 
 if __name__ == "__main__":

@@ -119,7 +119,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   constexpr int FN = C::FN, FP = C::FP, L = C::L, NBI = C::NBI, STAGE = C::STAGE, ST = C::ST;
   constexpr int ES = sizeof(TE), CC = 64 / ES, PE = 16 / ES;
   constexpr int NST = C::NST * (ES == 4 ? 2 : 1);  // stores per wave per epilogue
-  static_assert(ES == 2 || EPI != 2, "fp32: forward and plain input-gradient epilogues");
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -280,13 +279,13 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // pair), OOB for out-of-image pixels and columns outside [c0, c1))
   auto r_base = [&](const Pos& e) {
     const long m0 = ((long)e.img * p.ho + e.y0 + wave * RPW) * p.wo + e.x0;
-    return (const bf16*)p.bnb_r + m0 * p.bnb_r_ld + p.bnb_r_off;
+    return (const TE*)p.bnb_r + m0 * p.bnb_r_ld + p.bnb_r_off;
   };
   auto r_off = [&](const Pos& e, int f, int q) {
     const int c = n0 + 32 * q + 8 * g;
     const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
     const bool ok = e.y0 + wave * RPW + rr < p.ho && e.x0 + col < p.wo && c >= p.bnb_c0 && c < p.bnb_c1;
-    return ok ? (unsigned)((((long)rr * p.wo + col) * p.bnb_r_ld + (c - p.bnb_c0)) * 2) : OOB;
+    return ok ? (unsigned)((((long)rr * p.wo + col) * p.bnb_r_ld + (c - p.bnb_c0)) * ES) : OOB;
   };
   auto compute = [&](int buf, bool pf, int ch) {
     const char* Ps = smem + buf * STAGE;
@@ -426,8 +425,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   };
 
   // EPI 2: r loaded through a buffer descriptor (out-of-range -> zeros), stores to
-  // dz or g by column (global stores; out-of-image pixels go to the sink)
-  auto epilogue_bnb = [&](const Pos& e) {
+  // dz or g by column (global stores; out-of-image pixels go to the sink).  bf16: g is
+  // rounded to bf16 first (as cnnitmo_bn_bwd_apply reads it from a bf16 buffer); fp32:
+  // r of one column pair at a time (two 16-byte pieces per (pixel, 8 channels)).
+  auto epilogue_bnb16 = [&](const Pos& e) {
     const int oh0 = e.y0 + wave * RPW;
     const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
     const long m0 = ((long)e.img * p.ho + oh0) * p.wo + e.x0;  // the wave's first pixel
@@ -479,6 +480,93 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       }
     }
     zero_acc();
+  };
+
+  auto epilogue_bnb32 = [&](const Pos& e) {
+    const int oh0 = e.y0 + wave * RPW;
+    const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
+    const long m0 = ((long)e.img * p.ho + oh0) * p.wo + e.x0;  // the wave's first pixel
+    const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
+    constexpr int RQ = ES == 2 ? FP : 1;  // column pairs whose r is in flight at once
+    constexpr int RP = ES == 2 ? 1 : 2;   // 16-byte r pieces per (pixel, 8 channels)
+    dma::i32x4 rv[FM][RQ][RP];
+    auto load_r = [&](int q0) {
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int qq = 0; qq < RQ; ++qq) {
+          const unsigned o = r_off(e, f, q0 + qq);
+#pragma unroll
+          for (int h2 = 0; h2 < RP; ++h2) rv[f][qq][h2] = __builtin_amdgcn_raw_buffer_load_b128(rs, o == OOB ? OOB : o + 16 * h2, 0, 0);
+        }
+      // (also retires the next item's DMA, issued during this item's first taps).  Pulling
+      // these pieces into L2 one item ahead by LDS-DMA into the sink measured 15-25 %
+      // slower on every fused dgrad (dec6-dec8), whether issued before or after the
+      // ring's pieces.  Non-temporal r loads and epilogue stores (to keep the patch
+      // lines in L2 for the next chunk) measured 1-4 % slower on levels 0-2.
+      dma::wait_vm<0>();
+    };
+    TE* __restrict__ O = (TE*)p.out;
+    TE* __restrict__ Z = (TE*)p.bnb_out;
+    if constexpr (ES == 2) load_r(0);
+#pragma unroll
+    for (int q = 0; q < FP; ++q) {
+      if constexpr (ES == 4) load_r(q);
+      const int qr = ES == 2 ? q : 0;
+      const int cl = 32 * q + 8 * g, c = n0 + cl;
+      const bool fz = c >= c0 && c < c1;
+      float ca[8], cb[8], ce[8];
+      lds8(par + cl, ca);
+      lds8(par + BN + cl, cb);
+      lds8(par + 2 * BN + cl, ce);
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
+        const bool ok = oh0 + rr < p.ho && e.x0 + col < p.wo;
+        const long m = m0 + (long)rr * p.wo + col;
+        float v[8], rf[8];
+        if constexpr (ES == 2) {
+          const bf16x8 rq = __builtin_bit_cast(bf16x8, rv[f][qr][0]);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) rf[k] = to_f32(rq[k]);
+        } else {
+          const f32x4 r0 = __builtin_bit_cast(f32x4, rv[f][qr][0]), r1 = __builtin_bit_cast(f32x4, rv[f][qr][RP - 1]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            rf[k] = r0[k];
+            rf[4 + k] = r1[k];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float gk = to_f32(from_f32<TE>(acc[f][2 * q + (k >> 2)][k & 3]));
+          const float r = rf[k];
+          if (fz) {
+            v[k] = to_f32(from_f32<TE>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f));
+            sa[q][k] += (ok && rr == 0) ? v[k] : 0.f;
+            sb[q][k] += (ok && rr == 1) ? v[k] : 0.f;
+          } else {
+            v[k] = gk;
+          }
+        }
+        TE* dp = fz ? Z + (size_t)m * cbn + (c - c0) : O + (size_t)m * p.out_ld + p.out_off + c;
+        if constexpr (ES == 2) {
+          uint4* dst = !ok ? h_sink + lane : reinterpret_cast<uint4*>(dp);
+          *dst = __builtin_bit_cast(uint4, pack8(v));
+        } else {
+          uint4* d0 = !ok ? h_sink + lane : reinterpret_cast<uint4*>(dp);
+          uint4* d1 = !ok ? h_sink + lane : reinterpret_cast<uint4*>(dp + 4);
+          *d0 = __builtin_bit_cast(uint4, f32x4{v[0], v[1], v[2], v[3]});
+          *d1 = __builtin_bit_cast(uint4, f32x4{v[4], v[5], v[6], v[7]});
+        }
+      }
+    }
+    zero_acc();
+  };
+
+  auto epilogue_bnb = [&](const Pos& e) {
+    if constexpr (ES == 2) epilogue_bnb16(e);
+    else epilogue_bnb32(e);
   };
 
   if constexpr (RES) {  // the resident weights: every chunk's pieces, then a full drain
@@ -629,8 +717,7 @@ int halo_ncu() {
 }
 
 // conv3x3 stride 1 'same' (forward or input-gradient), 64-byte chunks (32 bf16 / 16 fp32
-// channels); fp32: the forward (EPI 1, with BN sums for training) and the plain input
-// gradient (EPI 0), one source
+// channels); fp32: one source (forward with BN sums, plain and fused input gradients)
 bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_HALO");
@@ -645,7 +732,7 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   if (!en || (f32 && !en32)) return false;
   if (f32) {
     if (a.cin % 16 || a.a_ld % 4 || a.a_off % 4 || a.out_ld % 4 || a.out_off % 4) return false;
-    if (a.a2 || a.bnb_out) return false;
+    if (a.a2) return false;
   } else if (a.cin % 32 || a.a_ld % 8 || a.a_off % 8 || a.out_ld % 8 || a.out_off % 8) {
     return false;
   }
@@ -704,6 +791,9 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
   if (f32 && pl.epi == 1) {
     if (pl.bn == 64) launch_cfg<float, 64, 1>(h, pl.res, grid, s);
     else launch_cfg<float, 32, 1>(h, pl.res, grid, s);
+  } else if (f32 && pl.epi == 2) {
+    if (pl.bn == 64) launch_cfg<float, 64, 2>(h, pl.res, grid, s);
+    else launch_cfg<float, 32, 2>(h, pl.res, grid, s);
   } else if (f32) {
     if (pl.bn == 64) launch_cfg<float, 64, 0>(h, pl.res, grid, s);
     else launch_cfg<float, 32, 0>(h, pl.res, grid, s);

@@ -514,8 +514,9 @@ extern "C" long cnnitmo_conv3x3_dgrad_bn_rows(int dtype, int n, int h, int w, in
                                               int c1) {
   FwdArgs a = dgrad_bn_args(n, h, w, cout, cin);
   a.bnb_c0 = c0; a.bnb_c1 = c1; a.bnb_out = (void*)1; a.bnb_r_ld = 8;
-  if (dtype != CNNITMO_BF16 || !halo_handles(a)) return 0;
-  return halo_stat_rows(a);
+  const bool f32 = dtype == CNNITMO_F32;
+  if ((dtype != CNNITMO_BF16 && !f32) || !halo_handles(a, f32)) return 0;
+  return halo_stat_rows(a, f32);
 }
 
 // Name of the kernel cnnitmo_conv3x3_dgrad_bn launches for these sizes (for profiles).
@@ -523,8 +524,9 @@ extern "C" const char* cnnitmo_conv3x3_dgrad_bn_kernel_name(int dtype, int n, in
                                                             int c0, int c1) {
   FwdArgs a = dgrad_bn_args(n, h, w, cout, cin);
   a.bnb_c0 = c0; a.bnb_c1 = c1; a.bnb_out = (void*)1; a.bnb_r_ld = 8;
-  if (dtype != CNNITMO_BF16 || !halo_handles(a)) return "";
-  return halo_name(a);
+  const bool f32 = dtype == CNNITMO_F32;
+  if ((dtype != CNNITMO_BF16 && !f32) || !halo_handles(a, f32)) return "";
+  return halo_name(a, f32);
 }
 
 extern "C" int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h, int w, int cout,
@@ -537,10 +539,11 @@ extern "C" int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h,
   a.bnb_c0 = c0; a.bnb_c1 = c1; a.bnb_par = parity ? 1 : 0;
   a.bnb_coef = coef; a.bnb_r = r; a.bnb_r_ld = r_ld; a.bnb_r_off = r_off; a.bnb_out = dz_out;
   a.stats = part;
-  CNN_REQUIRE(dtype == CNNITMO_BF16 && halo_handles(a), "conv3x3_dgrad_bn: unsupported sizes (bf16 halo only)");
+  const bool f32 = dtype == CNNITMO_F32;
+  CNN_REQUIRE((dtype == CNNITMO_BF16 || f32) && halo_handles(a, f32), "conv3x3_dgrad_bn: unsupported sizes (halo kernel only)");
   CNN_REQUIRE(coef && r && dz_out && part && (dx || (c0 == 0 && c1 == cin)),
               "conv3x3_dgrad_bn: missing buffers");
-  return launch_halo(a, (hipStream_t)stream, "conv3x3_dgrad_bn");
+  return launch_halo(a, (hipStream_t)stream, "conv3x3_dgrad_bn", f32);
 }
 
 extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int w, int cin,

@@ -50,6 +50,7 @@ def test_bench_spawns_ranks():
         pytest.skip("no GPU")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--height", "64", "--width", "96",
            "--batch", "2", "--steps", "2", "--warmup", "1", "--no-cpu", "--infer-batch", "1", "--bucket-mb", "0.5", "--k4-batch", "1", "--k4-steps", "1",
+           "--f32-train-batch", "1", "--f32-train-steps", "1",
            "--ns-batch", "2"]
     r = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -64,6 +65,9 @@ def test_bench_spawns_ranks():
     assert res["fp32_infer"]["config"]["global_batch"] == 2
     assert res["fp32_infer_b32"]["config"]["global_batch"] == 4
     assert res["k4_train"]["config"]["global_batch"] == 2 and res["k4_train"]["config"]["parallelism"] == "dp2"
+    assert res["fp32_train"]["config"]["global_batch"] == 2 and res["fp32_train"]["dtype"] == "f32"
+    for leg in ("k4_train", "fp32_train", "fp32_infer"):
+        assert "roofline" in res[leg] and "error" not in res[leg], res[leg]
 
 
 def test_rccl_one_rank_fit_generator():

@@ -256,30 +256,33 @@ def test_pool_deferred_route_and_sums(dt, H, W):
     (160, 64, 16, 40, 32, 160, True),    # BN 32 blocks
     (192, 128, 16, 32, 64, 192, True),   # concat [skip 64 | up 128] -> BN 64 blocks
     (128, 64, 17, 33, 0, 128, False)])
-def test_conv3x3_dgrad_bn_fused(cin, cout, H, W, c0, c1, par):
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+def test_conv3x3_dgrad_bn_fused(cin, cout, H, W, c0, c1, par, dt):
     """cnnitmo_conv3x3_dgrad_bn == conv3x3_dgrad followed by bn_bwd_apply on the
     fused column range (same coefficients, r read from a concat-style view);
-    columns outside the range are the plain input gradient."""
+    columns outside the range are the plain input gradient.  fp32: the halo kernel's
+    fp32 fused epilogue (fp32 training, 16-channel chunks)."""
     from cnn_itmo_amd import ops
     from cnn_itmo_amd import _lib as L
     rng = np.random.default_rng(cin + c0 + H)
-    N, d, c = 2, DT["bf16"], c1 - c0
+    N, d, c = 2, DT[dt], c1 - c0
+    T = TDT[dt]
     w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
-    wf = torch.empty(w.size, dtype=torch.bfloat16, device="cuda")
-    wflip = torch.empty(w.size, dtype=torch.bfloat16, device="cuda")
+    wf = torch.empty(w.size, dtype=T, device="cuda")
+    wflip = torch.empty(w.size, dtype=T, device="cuda")
     ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cin, wf, wflip)
-    dz = dev(rng.standard_normal((N, H, W, cout)).astype(np.float32), "bf16").reshape(-1)
-    rb = dev(np.maximum(rng.standard_normal((N, H, W, cin)), 0).astype(np.float32), "bf16").reshape(-1)
+    dz = dev(rng.standard_normal((N, H, W, cout)).astype(np.float32), dt).reshape(-1)
+    rb = dev(np.maximum(rng.standard_normal((N, H, W, cin)), 0).astype(np.float32), dt).reshape(-1)
     rv = ops.View(rb, N, H, W, c, cin, c0)
     coef = cu(rng.standard_normal(3 * c).astype(np.float32))
     P = N * H * W
     # unfused reference path
-    g = torch.zeros(P * cin, dtype=torch.bfloat16, device="cuda")
+    g = torch.zeros(P * cin, dtype=T, device="cuda")
     ops.conv3x3_dgrad(d, dz, N, H, W, cout, wflip, cin, ops.View(g, N, H, W, cin, cin, 0))
     rows = ops.bn_bwd_rows(P, c)
     np_ = 4 if par else 1
     pref = torch.empty(rows * np_ * c, device="cuda")
-    zref = torch.empty(P * c, dtype=torch.bfloat16, device="cuda")
+    zref = torch.empty(P * c, dtype=T, device="cuda")
     ops.bn_bwd_apply(d, ops.View(g, N, H, W, c, cin, c0), rv, c, coef, L.PARITY if par else 0, 0, 0, zref, pref)
     sref = torch.empty(np_ * c, device="cuda")
     ops.colsum(pref, rows, np_ * c, 1, sref)
@@ -287,17 +290,19 @@ def test_conv3x3_dgrad_bn_fused(cin, cout, H, W, c0, c1, par):
     frows = ops.conv3x3_dgrad_bn_rows(d, N, H, W, cout, cin, c0, c1)
     assert frows > 0
     whole = c0 == 0 and c1 == cin
-    dx = None if whole else ops.View(torch.zeros(P * cin, dtype=torch.bfloat16, device="cuda"), N, H, W, cin, cin)
-    zf = torch.empty(P * c, dtype=torch.bfloat16, device="cuda")
+    dx = None if whole else ops.View(torch.zeros(P * cin, dtype=T, device="cuda"), N, H, W, cin, cin)
+    zf = torch.empty(P * c, dtype=T, device="cuda")
     pf = torch.empty(frows * np_ * c, device="cuda")
     ops.conv3x3_dgrad_bn(d, dz, N, H, W, cout, wflip, cin, dx, c0, c1, coef, rv, zf, pf, par)
     sf = torch.empty(np_ * c, device="cuda")
     ops.colsum(pf, frows, np_ * c, 1, sf)
     torch.cuda.synchronize()
     a, b = host(zf), host(zref)
-    # same bf16 g and formula; an fp32 contraction difference may flip one bf16 rounding
-    assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())
-    assert np.mean(a != b) < 1e-3
+    if dt == "f32":  # the same fp32 g and formula (up to an fma contraction)
+        assert np.abs(a - b).max() <= 1e-5 * max(1.0, np.abs(b).max())
+    else:  # same bf16 g and formula; an fp32 contraction difference may flip one bf16 rounding
+        assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())
+        assert np.mean(a != b) < 1e-3
     np.testing.assert_allclose(host(sf), host(sref), rtol=1e-4, atol=1e-2)
     if not whole:
         gx = host(dx.buf).reshape(P, cin)

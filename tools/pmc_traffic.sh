@@ -13,7 +13,7 @@ run() {  # tag shape-key bench-args...
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "$shape" > "$R/gpurun_out/pmc_${tag}_$c.shape"
     timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc_${tag}_$c" -o run -- \
-      python3 "$R/bench.py" --no-cpu --steps 1 --warmup 0 --k4-batch 0 --infer-batch 0 --ns-batch 0 "$@" \
+      python3 "$R/bench.py" --no-cpu --steps 1 --warmup 0 --k4-batch 0 --infer-batch 0 --ns-batch 0 --f32-train-batch 0 "$@" \
       > "$R/gpurun_out/pmc_${tag}_$c.log" 2>&1
   done
 }

@@ -41,9 +41,9 @@ bench)
   cat "$O/${tag}_bench.json" ;;
 evidence)
   bash "$R/tools/pmc_traffic.sh"
-  bash "$R/tools/profile_round.sh" "$tag" --steps 5 --warmup 2 --infer-batch 0 --ns-batch 0 --k4-batch 0
+  bash "$R/tools/profile_round.sh" "$tag" --steps 5 --warmup 2 --infer-batch 0 --ns-batch 0 --k4-batch 0 --f32-train-batch 0
   bash "$R/tools/profile_round.sh" "${tag}_4k" --height 2160 --width 3840 --batch 8 --steps 5 --warmup 2 \
-    --infer-batch 0 --ns-batch 0 --k4-batch 0
+    --infer-batch 0 --ns-batch 0 --k4-batch 0 --f32-train-batch 0
   cd "$R"
   $T 900 python3 bench.py > "$O/${tag}_bench.json" 2> "$O/${tag}_bench.err"
   cat "$O/${tag}_bench.json" ;;
