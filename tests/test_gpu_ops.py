@@ -141,8 +141,9 @@ def test_conv_affine_inference_epilogue(dt, H, W):
                                           # bf16 weight-stationary kernel: fwd at 32 column blocks
                                           # (512 -> 512), dgrad at BN 128 (256 <- 128); ragged tiles
                                           (512, 512, 3, 7), (256, 128, 7, 9),
-                                          # a 1024-deep gradient (up7's shape: the implicit GEMM)
-                                          (512, 256, 5, 7),
+                                          # 1024 / 2048-deep gradients (up7 / up6: tconv_kc, weight
+                                          # chunks through LDS; ragged 256-pixel passes, 2 or 4 blocks)
+                                          (512, 256, 5, 7), (512, 256, 17, 33), (256, 512, 9, 31),
                                           # bf16 row-streaming wgrad: 4 rows per workgroup, 2 strips
                                           (512, 512, 16, 40)])
 def test_tconv(dt, cin, cout, H, W):
