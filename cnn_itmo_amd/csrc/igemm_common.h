@@ -188,3 +188,8 @@ const char* wgrad_halo_name(int n, int h, int w, int cin, int cout, bool cat = f
 int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n, int h, int w, int cin,
                       int cout, float* ws, size_t ws_bytes, hipStream_t s, const bf16* x2 = nullptr,
                       long x2_ld = 0, int x2_off = 0);
+// the same walk in fp32 (v_mfma_f32_16x16x4_f32), for fp32 training
+size_t wgrad_halo_f32_ws_bytes(int n, int h, int w, int cin, int cout);
+const char* wgrad_halo_f32_name(int n, int h, int w, int cin, int cout);
+int launch_wgrad_halo_f32(const float* x, long x_ld, int x_off, const float* dz, int n, int h, int w, int cin,
+                          int cout, float* ws, size_t ws_bytes, hipStream_t s);

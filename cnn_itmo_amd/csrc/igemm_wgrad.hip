@@ -486,7 +486,9 @@ extern "C" size_t cnnitmo_wgrad_workspace_bytes(int dtype, int n, int h, int w, 
     if (ntaps == 9) b = std::max(b, wgrad_halo_ws_bytes(n, h, w, cin, cout));
     return b;
   }
-  return ws_bytes_for<float>(P, cout, cin, ntaps);
+  size_t b = ws_bytes_for<float>(P, cout, cin, ntaps);
+  if (ntaps == 9) b = std::max(b, wgrad_halo_f32_ws_bytes(n, h, w, cin, cout));
+  return b;
 }
 
 extern "C" size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h, int w, int cin,
@@ -529,6 +531,17 @@ extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld,
   if (dtype == CNNITMO_BF16 && ntaps == 9) {
     const int splits = launch_wgrad_halo((const bf16*)x, x_ld, x_off, (const bf16*)dz, n, h, w, cin, cout,
                                          (float*)workspace, ws_bytes, s);
+    if (splits > 0) {
+      int rc = cnnitmo_check_launch("conv_wgrad");
+      if (rc) return rc;
+      const long slab = (long)cout * 9 * cin;
+      slab_reduce((const float*)workspace, slab, splits, cout, 9 * cin, cols_out, dw, f, s);
+      return cnnitmo_check_launch("conv_wgrad");
+    }
+  }
+  if (dtype == CNNITMO_F32 && ntaps == 9) {
+    const int splits = launch_wgrad_halo_f32((const float*)x, x_ld, x_off, (const float*)dz, n, h, w, cin, cout,
+                                             (float*)workspace, ws_bytes, s);
     if (splits > 0) {
       int rc = cnnitmo_check_launch("conv_wgrad");
       if (rc) return rc;
@@ -632,6 +645,10 @@ extern "C" const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, in
   if (dtype == CNNITMO_BF16 && ntaps == 4) {
     const char* tn = wgrad_tconv_name(n, h, w, cin, cout);
     if (tn[0]) return tn;
+  }
+  if (dtype == CNNITMO_F32 && ntaps == 9) {
+    const char* fn = wgrad_halo_f32_name(n, h, w, cin, cout);
+    if (fn[0]) return fn;
   }
   const long P = (long)n * h * w;
   static thread_local char buf[80];

@@ -305,6 +305,206 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
       }
 }
 
+// ---- fp32 (the fp32 training path, Keras' own precision; main.py:126-132) ---------
+// The same sliding-window walk with fp32 rows and v_mfma_f32_16x16x4_f32.  There is no
+// transposed LDS read for 32-bit elements, so a lane builds each 16-byte fragment (four
+// 16x16x4 MFMAs, k = pixel 4e + g) from four ds_read_b32 of consecutive pixel rows; the
+// 64-byte channel blocks of a row are XOR-swizzled by row parity (igemm_wgrad's f_off), so
+// the two rows a 32-lane half reads land on disjoint banks.  fp32 MFMA runs at 1/16 of the
+// bf16 rate, so neither the LDS reads nor the row DMA come close to binding; the point is
+// reading every x row once instead of once per tap (the implicit GEMM re-gathers x nine
+// times).  Blocks of 32 / 64 output x 32 / 64 input channels, 64-pixel strips, one row per
+// barrier step, two row groups ahead; 3 x (BM/32) x (BN/32) waves of 32 x 32 tiles.
+template <int C> __device__ __forceinline__ int ffo(int row, int col) {
+  return row * (C * 4) + ((((col >> 4) ^ (row & 1))) << 6) + ((col & 15) << 2);
+}
+
+template <int BM, int BN>
+struct WF32Cfg {
+  static constexpr int WM = BM / 32, WN = BN / 32, NWG = WM * WN, NW = 3 * NWG, NT = NW * 64;
+  static constexpr int TW = 64, XROWS = TW + 2, D = 2, R = 1;
+  static constexpr int XB = (XROWS * BN * 4 + 1023) / 1024, DB = TW * BM * 4 / 1024;
+  static constexpr int XS = D + R + 2, DS = D + R;
+  static constexpr int SMEM = ((XS + 1) * XB + DS * DB) * 1024;
+  static constexpr int LX = (XB + NW - 1) / NW, LD = (DB + NW - 1) / NW;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(3 * (BM / 32) * (BN / 32) * 64) void wgrad_halo_f32_kernel(const WHArgs p) {
+  using C = WF32Cfg<BM, BN>;
+  constexpr int NW = C::NW, TW = C::TW, XB = C::XB, DB = C::DB, XS = C::XS, DS = C::DS, LX = C::LX, LD = C::LD;
+  constexpr int D = C::D, WN = C::WN;
+  constexpr int FM = 2, FN = 2;  // 32 x 32 wave tiles
+  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  char* const xbase = smem;
+  char* const zrow = smem + XS * XB * 1024;
+  char* const dbase = zrow + XB * 1024;
+  const float* X = reinterpret_cast<const float*>(p.x);
+  const float* DZ = reinterpret_cast<const float*>(p.dz);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / C::NWG, wq = wave - wr * C::NWG;
+  const int wm = wq / WN, wn = wq % WN;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int cb = bid % (p.cbm * p.cbn);
+  bid /= p.cbm * p.cbn;
+  const int strip = bid % p.strips;
+  const int rs = bid / p.strips;
+  const int m0 = (cb / p.cbn) * BM, n0 = (cb % p.cbn) * BN;
+  const int x0 = strip * TW;
+  const long total_rows = (long)p.nimg * p.H;
+  const long g0 = (long)rs * p.rows_per;
+  const long g1 = g0 + p.rows_per < total_rows ? g0 + p.rows_per : total_rows;
+  const int nrows = (int)(g1 - g0);
+  const int split = rs * p.strips + strip;
+
+  // DMA geometry: LDS slot (row, piece pc') holds logical piece pc' ^ 4*(row & 1)
+  unsigned xoff[LX];
+  bool xact[LX];
+#pragma unroll
+  for (int q = 0; q < LX; ++q) {
+    const int ins = wave + q * NW;
+    xact[q] = ins < XB;
+    const int off = ins * 1024 + lane * 16;
+    const int row = off / (BN * 4), pos = off - row * (BN * 4);
+    const int col = ((pos >> 4) ^ ((row & 1) << 2)) * 4;
+    const int xx = x0 - 1 + row;
+    xoff[q] = row < C::XROWS && xx >= 0 && xx < p.W ? (unsigned)((row * p.x_ld + col) * 4) : dma::OOB;
+  }
+  unsigned doff[LD];
+  bool dact[LD];
+#pragma unroll
+  for (int q = 0; q < LD; ++q) {
+    const int ins = wave + q * NW;
+    dact[q] = ins < DB;
+    const int off = ins * 1024 + lane * 16;
+    const int row = off / (BM * 4), pos = off - row * (BM * 4);
+    const int col = ((pos >> 4) ^ ((row & 1) << 2)) * 4;
+    doff[q] = x0 + row < p.W ? (unsigned)((row * p.cout + col) * 4) : dma::OOB;
+  }
+  int nx = 0, nd = 0;
+#pragma unroll
+  for (int q = 0; q < LX; ++q) nx += xact[q] ? 1 : 0;
+#pragma unroll
+  for (int q = 0; q < LD; ++q) nd += dact[q] ? 1 : 0;
+
+  auto issue_x = [&](long g, int slot) {
+    char* S = xbase + slot * XB * 1024;
+    const bool ok = g >= 0 && g < total_rows;
+    const long e0 = ((long)g * p.W + x0 - 1) * p.x_ld + p.x_off + n0;
+    const i32x4 rsc = dma::rsrc((uintptr_t)X + (uintptr_t)(e0 * 4));
+#pragma unroll
+    for (int q = 0; q < LX; ++q)
+      if (xact[q]) dma::lds16(ok ? xoff[q] : dma::OOB, rsc, S + (wave + q * NW) * 1024);
+  };
+  auto issue_d = [&](long g, int slot) {
+    char* S = dbase + slot * DB * 1024;
+    const i32x4 rsc = dma::rsrc((uintptr_t)(DZ + ((size_t)g * p.W + x0) * p.cout + m0));
+#pragma unroll
+    for (int q = 0; q < LD; ++q)
+      if (dact[q]) dma::lds16(doff[q], rsc, S + (wave + q * NW) * 1024);
+  };
+
+  f32x4 acc[3][FM][FN];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15;
+  for (int i = tid; i < XB * 1024 / 16; i += C::NT)
+    *reinterpret_cast<uint4*>(zrow + i * 16) = uint4{0u, 0u, 0u, 0u};
+
+  int issued = 0;
+  int gq[D + 1];
+  int xslot_next = 0, dslot_next = 0;
+  auto issue_group = [&](int j) {
+    issue_d(g0 + j, dslot_next);
+    dslot_next = dslot_next + 1 == DS ? 0 : dslot_next + 1;
+    issue_x(g0 + j + 1, xslot_next);
+    xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+    issued += nd + nx;
+  };
+  issue_x(g0 - 1, xslot_next);
+  xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+  issue_x(g0, xslot_next);
+  xslot_next = xslot_next + 1 == XS ? 0 : xslot_next + 1;
+  issued += 2 * nx;
+#pragma unroll
+  for (int j = 0; j < D + 1; ++j) {
+    if (j < D && j < nrows) issue_group(j);
+    gq[j] = issued;
+  }
+  int xs0 = 0, ds0 = 0;
+  int y = (int)(g0 % p.H);
+  auto nxt = [](int sl, int n) { return sl + 1 == n ? 0 : sl + 1; };
+  for (int k = 0; k < nrows; ++k) {
+    dma::wait_vm_dyn(issued - gq[0]);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + D < nrows) issue_group(k + D);
+    gq[D] = issued;
+    {
+      const char* Ds = dbase + ds0 * DB * 1024;
+      const int xb = nxt(xs0, XS), xc = nxt(xb, XS);
+      const int xsr = wr == 0 ? xs0 : (wr == 1 ? xb : xc);
+      const char* Xs = (wr == 0 && y == 0) || (wr == 2 && y == p.H - 1) ? zrow : xbase + xsr * XB * 1024;
+#pragma unroll
+      for (int kk = 0; kk < TW / 16; ++kk) {
+        uint4 af[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int col = wm * 32 + i * 16 + li;
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = *reinterpret_cast<const float*>(Ds + ffo<BM>(kk * 16 + 4 * e + g, col));
+          af[i] = __builtin_bit_cast(uint4, v);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 3; ++s2) {
+          uint4 bfr[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int col = wn * 32 + j * 16 + li;
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = *reinterpret_cast<const float*>(Xs + ffo<BN>(kk * 16 + 4 * e + g + s2, col));
+            bfr[j] = __builtin_bit_cast(uint4, v);
+          }
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) Mma<float>::run(acc[s2][i][j], af[i], bfr[j]);
+        }
+      }
+    }
+    xs0 = nxt(xs0, XS);
+    ds0 = nxt(ds0, DS);
+    y = y + 1 == p.H ? 0 : y + 1;
+#pragma unroll
+    for (int q = 0; q < D; ++q) gq[q] = gq[q + 1];
+  }
+
+  float* __restrict__ O = p.out + (size_t)split * p.slab;
+#pragma unroll
+  for (int s2 = 0; s2 < 3; ++s2)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = m0 + wm * 32 + i * 16 + g * 4 + rr;
+        const int t = wr * 3 + s2;
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          O[(size_t)co * 9 * p.cin + t * p.cin + n0 + wn * 32 + j * 16 + li] = acc[s2][i][j][rr];
+      }
+}
+
 // Rows per barrier step.  Timing-only builds of the 64 x 96 block (dec6-dec9; garbage
 // results): no s_barrier -11 %, no vmcnt wait -11 %, no row DMA -15 %, none of the
 // three -24 % (1.15 -> 1.5 PF/s: the MFMA + fragment-read loop alone); prefetching 4
@@ -458,6 +658,47 @@ void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
                      a);
 }
 
+// fp32 plan: 32 / 64 x 32 / 64 blocks, 64-pixel strips, the row split of wh_plan's policy
+bool wh_plan_f32(int n, int h, int w, int cin, int cout, WHPlan& pl) {
+  static const int mode = [] {
+    const char* e = getenv("CNNITMO_WGRAD_HALO_F32");
+    return e ? atoi(e) : 1;
+  }();
+  if (!mode) return false;
+  pl.bm = cout % 64 == 0 ? 64 : (cout % 32 == 0 ? 32 : 0);
+  pl.bn = cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0);
+  if (!pl.bm || !pl.bn) return false;
+  pl.tw = 64;
+  pl.strips = (w + pl.tw - 1) / pl.tw;
+  pl.cbm = cout / pl.bm;
+  pl.cbn = cin / pl.bn;
+  const long rows = (long)n * h;
+  const long per = (long)pl.strips * pl.cbm * pl.cbn;
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      ncu = prop.multiProcessorCount;
+    if (ncu <= 0) ncu = 256;
+  }
+  const int xb = (66 * pl.bn * 4 + 1023) / 1024, db = 64 * pl.bm * 4 / 1024;
+  const int smem = (6 * xb + 3 * db) * 1024;  // WF32Cfg::SMEM
+  const long slots = (long)ncu * std::max(1, (160 * 1024) / smem);
+  long best = 1;
+  double best_eff = -1.0;
+  for (long r = 1; r <= 64 && r <= rows; ++r) {
+    const long blocks = per * r;
+    const long rounds = (blocks + slots - 1) / slots;
+    double eff = (double)blocks / (double)(rounds * slots);
+    if (blocks < slots / 2) eff *= 0.5;
+    if (eff > best_eff + 1e-3) { best_eff = eff; best = r; }
+  }
+  pl.rows_per = (rows + best - 1) / best;
+  pl.rsplits = (int)((rows + pl.rows_per - 1) / pl.rows_per);
+  return true;
+}
+
 }  // namespace
 
 size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout, bool cat) {
@@ -504,5 +745,44 @@ const char* wgrad_halo_name(int n, int h, int w, int cin, int cout, bool cat) {
   if (!wh_plan(n, h, w, cin, cout, pl, cat)) return "";
   static thread_local char buf[64];
   snprintf(buf, sizeof(buf), "wgrad_halo_kernel<%d,%d,%d%s>", pl.bm, pl.bn, pl.tw, cat ? ",cat" : "");
+  return buf;
+}
+
+// fp32: returns the slabs written (> 0) or -1 when this path does not apply.
+int launch_wgrad_halo_f32(const float* x, long x_ld, int x_off, const float* dz, int n, int h, int w, int cin,
+                          int cout, float* ws, size_t ws_bytes, hipStream_t s) {
+  WHPlan pl;
+  if (!wh_plan_f32(n, h, w, cin, cout, pl)) return -1;
+  if (x_ld % 4 || x_off % 4) return -1;
+  const size_t need = (size_t)pl.strips * pl.rsplits * cout * 9 * cin * 4;
+  if (!ws || ws_bytes < need) return -1;
+  WHArgs a;
+  memset(&a, 0, sizeof(a));
+  a.dz = (const bf16*)dz; a.cout = cout; a.x = (const bf16*)x; a.x_ld = x_ld; a.x_off = x_off;
+  a.nimg = n; a.H = h; a.W = w; a.cin = cin;
+  a.out = ws; a.slab = (long)cout * 9 * cin;
+  a.strips = pl.strips; a.cbm = pl.cbm; a.cbn = pl.cbn; a.rsplits = pl.rsplits; a.rows_per = pl.rows_per;
+  const unsigned grid = (unsigned)(pl.strips * pl.cbm * pl.cbn * pl.rsplits);
+#define WF(BMv, BNv)                                                                                        \
+  if (pl.bm == BMv && pl.bn == BNv) {                                                                    \
+    hipLaunchKernelGGL((wgrad_halo_f32_kernel<BMv, BNv>), dim3(grid), dim3(WF32Cfg<BMv, BNv>::NT), 0, s, a); \
+    return pl.strips * pl.rsplits;                                                                       \
+  }
+  WF(64, 64) WF(64, 32) WF(32, 64) WF(32, 32)
+#undef WF
+  return -1;
+}
+
+size_t wgrad_halo_f32_ws_bytes(int n, int h, int w, int cin, int cout) {
+  WHPlan pl;
+  if (!wh_plan_f32(n, h, w, cin, cout, pl)) return 0;
+  return (size_t)pl.strips * pl.rsplits * cout * 9 * cin * 4;
+}
+
+const char* wgrad_halo_f32_name(int n, int h, int w, int cin, int cout) {
+  WHPlan pl;
+  if (!wh_plan_f32(n, h, w, cin, cout, pl)) return "";
+  static thread_local char buf[64];
+  snprintf(buf, sizeof(buf), "wgrad_halo_kernel<f32,%d,%d,64>", pl.bm, pl.bn);
   return buf;
 }
