@@ -12,6 +12,8 @@
 #   bash tools/recipe.sh env      <tag> "<VAR=value>" <layers> <ops>  per-layer A/B under an environment switch
 #   bash tools/recipe.sh benchab  <tag> "<VAR=value>|<lib.so>" [bench args...]   bench A/B, interleaved twice
 #   bash tools/recipe.sh pmc      <tag> <layers> <ops> "<counters>"  one rocprofv3 --pmc pass over bench_layers
+#   bash tools/recipe.sh mfma     <tag> [bench args...]        MFMA-busy + GRBM_GUI_ACTIVE pass over one bench step
+#                                                              (post-process: python tools/mfma_busy.py <csv>)
 #
 # Variant libraries come from tools/build_variant.sh (CPU side, before the call).
 set -e
@@ -74,6 +76,11 @@ pmc)
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d "$O/pmc_$tag" -o run -- \
     python3 "$R/tools/bench_layers.py" --layers "$L" --ops "$P" --iters 1 > "$O/pmc_${tag}.log" 2>&1 ;;
+mfma)
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+    --output-format csv -d "$O/mfma_$tag" -o run -- python3 "$R/bench.py" --no-cpu --steps 1 --warmup 1 \
+    --infer-batch 0 --ns-batch 0 --k4-batch 0 --f32-train-batch 0 "$@" > "$O/mfma_${tag}.log" 2>&1 ;;
 *)
   echo "unknown recipe step: $cmd" >&2; exit 2 ;;
 esac
