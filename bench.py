@@ -117,7 +117,7 @@ class KernelTimer:
     def _wrap(self):
         ops = self.ops
         query = functools.lru_cache(maxsize=None)(ops.query)  # kernel names: one ctypes query per shape
-        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
+        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
                                            "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
                                            "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad")}
 
@@ -130,6 +130,15 @@ class KernelTimer:
             self._nb = (2 if dt == 1 else 4) * (x.p * x.c + x.p * out.c + 9 * x.c * out.c)
             return self._bracket(kname(dt, x.n, x.h, x.w, x.c, out.c, 0), fl, f"fwd {x.h}x{x.w} {x.c}->{out.c}", o["conv3x3_fwd"], dt, x, wt, bias,
                                  out, *a, **k)
+
+        def conv3x3_fwd_pool(dt, x, wt, bias, out, *a, **k):
+            fl = 2.0 * x.p * out.c * 9 * x.c
+            # + the pooled value and window index it writes (the stand-alone pool pass it replaces)
+            self._nb = (2 if dt == 1 else 4) * (x.p * x.c + x.p * out.c + 9 * x.c * out.c) + \
+                ((2 if dt == 1 else 4) + 1) * x.p * out.c // 4
+            nm = kname(dt, x.n, x.h, x.w, x.c, out.c, 0).replace(">", ",pool>")
+            return self._bracket(nm, fl, f"fwd+pool {x.h}x{x.w} {x.c}->{out.c}", o["conv3x3_fwd_pool"], dt, x, wt,
+                                 bias, out, *a, **k)
 
         def conv3x3_fwd_cat(dt, x1, x2, wt, bias, out, *a, **k):
             cin = x1.c + x2.c
@@ -203,7 +212,8 @@ class KernelTimer:
             return self._bracket(wname(dt, 4, x.n, x.h, x.w, x.c, cout), fl, f"t.wgrad {x.h}x{x.w} {x.c}->{cout}", o["tconv_wgrad"],
                                  dt, x, dout, cout, dk, *a, **k)
 
-        for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_fwd_cat", conv3x3_fwd_cat), ("conv_wgrad_cat", conv_wgrad_cat),
+        for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_fwd_pool", conv3x3_fwd_pool),
+                     ("conv3x3_fwd_cat", conv3x3_fwd_cat), ("conv_wgrad_cat", conv_wgrad_cat),
                      ("conv3x3_dgrad", conv3x3_dgrad),
                      ("conv3x3_dgrad_bn", conv3x3_dgrad_bn), ("tconv_fwd", tconv_fwd),
                      ("tconv_dgrad", tconv_dgrad), ("tconv_dgrad_bn", tconv_dgrad_bn), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),

@@ -89,8 +89,8 @@ template <int BN, bool RES> struct HCfg {
   static constexpr int ST = 2;
   static constexpr int WRES = ST * STAGE;                   // resident weights (RES)
   static constexpr int SCR = WRES + (RES ? RCH * BPC * 1024 : 0);  // 1 KiB sink for the padding pieces
-  static constexpr int PAR = SCR + 1024;    // [3][BN] fp32 epilogue parameters
-  static constexpr int UTB = PAR + 3 * BN * 4;  // [BN][8] fp32 border table
+  static constexpr int PAR = SCR + 1024;    // [4][BN] fp32 epilogue parameters (bias, scale, shift, pool mode)
+  static constexpr int UTB = PAR + 4 * BN * 4;  // [BN][8] fp32 border table
   static constexpr int SMEM = UTB + BN * 8 * 4;
   static constexpr int NST = FM * FP;  // 16-byte stores per wave per epilogue
   static_assert(SMEM <= 160 * 1024, "LDS");
@@ -113,12 +113,24 @@ struct HaloArgs {
 // fragment as four 16x16x4 f32 MFMAs, so the fragment reads, the swizzle and the
 // operand-swapped register layout are the same.  fp32 stores take two 16-byte stores per
 // (pixel, 8 channels).
-template <typename TE, int BN, int EPI, bool RES>
+// POOL (EPI 1): the 2x2 MaxPooling2D of the stored output rides on the epilogue (SURVEY 7,
+// hard part 2): a wave's two tile rows are a row of 2x2 windows and the window's right
+// column is the neighbouring lane (DPP quad_perm xor 1), so the even lanes write the
+// pooled value and its window index (first maximum, window order (0,0),(0,1),(1,0),(1,1),
+// on the values as stored).  Training stores r = relu(conv) with the BN folded into the
+// consumers; y = r*s + h is monotone in r with the sign of s = gamma * invstd, i.e. of gamma
+// (known before the batch statistics), so the pooled y is s * (max r) + h where gamma > 0
+// and s * (min r) + h where gamma < 0: the kernel pools r by the per-channel mode sign(gamma)
+// (pool_sign), and the pooled value is itself a folded value.  Inference stores y (AFFINE)
+// and pools it by its maximum.
+template <typename TE, int BN, int EPI, bool RES, bool POOL = false>
 __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   using C = HCfg<BN, RES>;
   constexpr int FN = C::FN, FP = C::FP, L = C::L, NBI = C::NBI, STAGE = C::STAGE, ST = C::ST;
   constexpr int ES = sizeof(TE), CC = 64 / ES, PE = 16 / ES;
-  constexpr int NST = C::NST * (ES == 4 ? 2 : 1);  // stores per wave per epilogue
+  static_assert(!POOL || (EPI == 1 && RPW % 2 == 0), "pooling: the forward epilogue, whole window rows per wave");
+  // stores per wave per epilogue (+ POOL: a value and an index store per window row and column block)
+  constexpr int NST = C::NST * (ES == 4 ? 2 : 1) + (POOL ? FP * (RPW / 2) * FMR * (ES == 4 ? 3 : 2) : 0);
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -145,10 +157,11 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // the workgroup's epilogue parameters (ordered before any epilogue by the ring barrier)
   if constexpr (EPI == 1) {
     const bool aff = p.flags & CNNITMO_AFFINE;
-    for (int i = tid; i < 3 * BN; i += NT) {
+    for (int i = tid; i < 4 * BN; i += NT) {
       const int k = i / BN, c = n0 + i % BN;
+      const float sg = k == 3 && p.pool_sign ? p.pool_sign[c] : 1.f;
       par[i] = k == 0 ? (p.bias ? p.bias[c] : 0.f) : k == 1 ? (aff ? p.aff_scale[c] : 1.f)
-                                                            : (aff ? p.aff_shift[c] : 0.f);
+             : k == 2 ? (aff ? p.aff_shift[c] : 0.f) : (sg > 0.f ? 1.f : (sg < 0.f ? -1.f : 0.f));
     }
     for (int i = tid; i < 8 * BN; i += NT) utb[i] = p.border ? p.border[(size_t)n0 * 8 + i] : 0.f;
   } else if constexpr (EPI == 2) {
@@ -353,17 +366,29 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE;
     const bool bt = EPI == 1 && p.border && (oh0 == 0 || oh0 + RPW >= p.ho || e.x0 == 0 || e.x0 + TW >= p.wo);
     dma::i32x4 pk[LINES ? FP : 1][LINES ? FM : 1];
+    static_assert(!(LINES && POOL), "pooling stores from the fragment layout");
+    // POOL: the wave's pooled rows start at (oh0 / 2, x0 / 2) of the [n][ho/2][wo/2] output
+    const size_t pofs = (((size_t)e.img * (p.ho / 2) + oh0 / 2) * (p.wo / 2) + e.x0 / 2) * p.pool_ld + n0;
+    const __amdgpu_buffer_rsrc_t ps = dma::brsrc(POOL ? (const TE*)p.pool_out + pofs : obase);
+    const __amdgpu_buffer_rsrc_t pis = dma::brsrc(POOL ? (const unsigned char*)p.pool_idx + pofs : (const unsigned char*)obase);
+    // POOL: the window rows' values as stored (bf16: the packed store operand, 4 VGPRs a row)
+    float vr[ES == 4 ? 2 : 1][8];
+    dma::i32x4 vrp[2];
 #pragma unroll
     for (int q = 0; q < FP; ++q) {
       const int cl = 32 * q + 8 * g;  // the lane's first column in the block
-      float bj[8], sj[8], hj[8];
+      float bj[8], sj[8], hj[8], md[8];
       if constexpr (EPI == 1) {
         lds8(par + cl, bj);
         lds8(par + BN + cl, sj);
         lds8(par + 2 * BN + cl, hj);
       }
+      if constexpr (POOL) lds8(par + 3 * BN + cl, md);
 #pragma unroll
-      for (int f = 0; f < FM; ++f) {
+      for (int fi = 0; fi < FM; ++fi) {
+        // POOL: fragments in window order (pooled row rp, column block cb, tile row 2rp+rl)
+        const int rp = fi / (2 * FMR), cb = (fi % (2 * FMR)) / 2, rl = fi % 2;
+        const int f = POOL ? (2 * rp + rl) * FMR + cb : fi;
         const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
         const int oh = oh0 + rr, ow = e.x0 + col;
         const bool ok = oh < p.ho && ow < p.wo;
@@ -401,7 +426,66 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, hi), os, ok ? off + 16 : OOB, 0, 0);
         } else {
           const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 2);
-          __builtin_amdgcn_raw_buffer_store_b128(pack8(v), os, ok ? off : OOB, 0, 0);
+          const dma::i32x4 pk8 = pack8(v);
+          __builtin_amdgcn_raw_buffer_store_b128(pk8, os, ok ? off : OOB, 0, 0);
+          if constexpr (POOL) vrp[rl] = pk8;
+        }
+        if constexpr (POOL) {
+          if constexpr (ES == 4) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) vr[rl][k] = v[k];
+          }
+          if (rl == 1) {  // window row complete: (0,0),(0,1) = row 0 here and right; (1,0),(1,1) = row 1
+            float pv[8], w0[8], w1[8], w2[8], w3[8];
+            if constexpr (ES == 4) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                w0[k] = vr[0][k];
+                w2[k] = vr[1][k];
+                w1[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w0[k]), 0xB1, 0xF, 0xF, false));
+                w3[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w2[k]), 0xB1, 0xF, 0xF, false));
+              }
+            } else {  // the neighbour's packed rows by DPP (4 dwords each), then unpacked
+              dma::i32x4 n0v, n1v;
+#pragma unroll
+              for (int d = 0; d < 4; ++d) {
+                n0v[d] = __builtin_amdgcn_update_dpp(0, vrp[0][d], 0xB1, 0xF, 0xF, false);
+                n1v[d] = __builtin_amdgcn_update_dpp(0, vrp[1][d], 0xB1, 0xF, 0xF, false);
+              }
+              const bf16x8 b0 = __builtin_bit_cast(bf16x8, vrp[0]), b1 = __builtin_bit_cast(bf16x8, n0v);
+              const bf16x8 b2 = __builtin_bit_cast(bf16x8, vrp[1]), b3 = __builtin_bit_cast(bf16x8, n1v);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                w0[k] = to_f32(b0[k]);
+                w1[k] = to_f32(b1[k]);
+                w2[k] = to_f32(b2[k]);
+                w3[k] = to_f32(b3[k]);
+              }
+            }
+            unsigned pa[2] = {0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float t0 = w0[k], t1 = w1[k], t2 = w2[k], t3 = w3[k];
+              float best = t0, kb = md[k] * t0;
+              unsigned a = 0;
+              if (md[k] * t1 > kb) { kb = md[k] * t1; best = t1; a = 1; }
+              if (md[k] * t2 > kb) { kb = md[k] * t2; best = t2; a = 2; }
+              if (md[k] * t3 > kb) { best = t3; a = 3; }
+              pv[k] = best;
+              pa[k >> 2] |= a << (8 * (k & 3));
+            }
+            const bool pok = (pxl & 1) == 0 && oh0 + 2 * rp < p.ho && e.x0 + cb * 16 + pxl < p.wo;
+            const unsigned pe = (unsigned)((rp * (p.wo / 2) + cb * 8 + (pxl >> 1)) * p.pool_ld + cl);  // elements
+            if constexpr (ES == 4) {
+              const float4 lo = {pv[0], pv[1], pv[2], pv[3]}, hi = {pv[4], pv[5], pv[6], pv[7]};
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, lo), ps, pok ? pe * 4 : OOB, 0, 0);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, hi), ps, pok ? pe * 4 + 16 : OOB, 0, 0);
+            } else {
+              __builtin_amdgcn_raw_buffer_store_b128(pack8(pv), ps, pok ? pe * 2 : OOB, 0, 0);
+            }
+            typedef int i32x2_ __attribute__((ext_vector_type(2)));
+            __builtin_amdgcn_raw_buffer_store_b64(i32x2_{(int)pa[0], (int)pa[1]}, pis, pok ? pe : OOB, 0, 0);
+          }
         }
       }
     }
@@ -739,6 +823,8 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   if (a.a2 && (a.cin1 % 32 || a.cin1 <= 0 || a.cin1 >= a.cin || a.a2_ld % 8 || a.a2_off % 8 || a.bnb_out))
     return false;
   if (a.ntaps != 9 || a.scale != 1 || a.scatter || a.hs != a.ho || a.ws != a.wo) return false;
+  if (a.pool_out && (a.a2 || a.bnb_out || a.ho % 2 || a.wo % 2 || a.pool_ld % 8 || a.pool_ld < a.N || !a.pool_idx))
+    return false;
   pl.bn = a.N % 64 == 0 ? 64 : (a.N % 32 == 0 ? 32 : 0);
   if (!pl.bn || a.N / pl.bn > halo_ncu() / 8) return false;
   if (a.bnb_out) {  // fused BN backward (input gradient)
@@ -760,6 +846,13 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
 
 template <typename T, int BN, int EPI>
 void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
+  if constexpr (EPI == 1) {
+    if (h.f.pool_out) {
+      if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
+      else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true>), dim3(grid), dim3(NT), 0, s, h);
+      return;
+    }
+  }
   if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true>), dim3(grid), dim3(NT), 0, s, h);
   else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false>), dim3(grid), dim3(NT), 0, s, h);
 }

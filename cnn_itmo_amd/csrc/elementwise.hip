@@ -631,7 +631,9 @@ __global__ void maxpool_bwd_kernel(const T* __restrict__ dy, const uint8_t* __re
 // cnnitmo_bn_consumer_sums): sum_p dyp[p] and sum_p dyp[p] * rhat[argmax(p)].
 // The 2x2 window of r is read whole (two coalesced pixel pairs) and the argmax
 // element selected per channel.
-template <typename T>
+// PRE: r is the pooled r itself ([Pp][C] dense: the producer's epilogue wrote r at the
+// window index, cnnitmo_conv3x3_fwd_pool), so no window is read and idx is not needed.
+template <typename T, bool PRE = false>
 __global__ void pool_bnsums_kernel(const T* __restrict__ dyp, const uint8_t* __restrict__ idx, int H, int W,
                                    long Pp, int C, const T* __restrict__ r, long r_ld, int r_off,
                                    const float* __restrict__ mean, const float* __restrict__ inv,
@@ -654,6 +656,15 @@ __global__ void pool_bnsums_kernel(const T* __restrict__ dyp, const uint8_t* __r
       const int ho = rem / Wo, wo = rem - ho * Wo;
       float g[VE], rw[4][VE];
       Pack16<T>::load(dyp + (size_t)po * C + c0, g);
+      if constexpr (PRE) {
+        Pack16<T>::load(r + (size_t)po * C + c0, rw[0]);
+#pragma unroll
+        for (int e = 0; e < VE; ++e) {
+          acc[0][e] += g[e];
+          acc[1][e] += g[e] * (rw[0][e] - mu[e]) * is[e];
+        }
+        continue;
+      }
       uint8_t arg[VE];
       load_args<VE>(idx + (size_t)po * C + c0, arg);
 #pragma unroll
@@ -671,6 +682,23 @@ __global__ void pool_bnsums_kernel(const T* __restrict__ dyp, const uint8_t* __r
     }
   }
   block_reduce_rows<VE, 2>(acc, C, part);
+}
+
+extern "C" int cnnitmo_pool_bnsums_pooled(int dtype, const void* dyp, const void* pr, int n, int h, int w, int c,
+                                          const float* mean, const float* invstd, float* part, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int VE = dtype == CNNITMO_BF16 ? 8 : 4;
+  CNN_REQUIRE(c % 8 == 0 && c / VE <= 256 && dyp && pr, "pool_bnsums_pooled: unsupported channel count %d", c);
+  const long Pp = (long)n * (h / 2) * (w / 2);
+  CNN_REQUIRE(Pp < (1L << 31), "pool_bnsums_pooled: too many pixels");
+  const int G = cnnitmo_bn_bwd_rows(Pp, c);
+  if (dtype == CNNITMO_BF16)
+    hipLaunchKernelGGL((pool_bnsums_kernel<bf16, true>), dim3(G), dim3(256), 0, s, (const bf16*)dyp, nullptr, h, w,
+                       Pp, c, (const bf16*)pr, (long)c, 0, mean, invstd, part);
+  else
+    hipLaunchKernelGGL((pool_bnsums_kernel<float, true>), dim3(G), dim3(256), 0, s, (const float*)dyp, nullptr, h,
+                       w, Pp, c, (const float*)pr, (long)c, 0, mean, invstd, part);
+  return cnnitmo_check_launch("pool_bnsums_pooled");
 }
 
 extern "C" int cnnitmo_maxpool2x2_fwd(int dtype, const void* x, int x_ld, int x_off, int n, int h,

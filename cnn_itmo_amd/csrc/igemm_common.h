@@ -43,6 +43,13 @@ struct FwdArgs {
   long a2_ld;
   int a2_off;
   int cin1;
+  // the output's 2x2 MaxPooling2D fused into the forward epilogue (halo kernel, EPI 1):
+  // pooled values [n][ho/2][wo/2] x pool_ld, window index bytes (same layout), per-channel
+  // mode sign(pool_sign[c]) (null: max)
+  void* pool_out;
+  long pool_ld;
+  unsigned char* pool_idx;
+  const float* pool_sign;
 };
 
 // Out-of-bounds-tap correction for a folded BN shift (see cnnitmo_fold_conv3x3):

@@ -376,6 +376,45 @@ extern "C" int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off
   return dispatch(dtype, a, stream, "conv3x3_fwd");
 }
 
+extern "C" int cnnitmo_conv3x3_fwd_pool(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w,
+                                        int cin, const void* wt, const float* bias, int cout, void* out, int out_ld,
+                                        int out_off, int flags, const float* aff_scale, const float* aff_shift,
+                                        float* stat_part, const float* border, void* pool_out, int pool_ld,
+                                        unsigned char* pool_idx, const float* pool_sign, void* stream) {
+  FwdArgs a = base_args();
+  a.a = x; a.a_ld = x_ld; a.a_off = x_off;
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cin; a.b = wt; a.N = cout; a.M = (long)n * h * w;
+  a.bias = bias; a.out = out; a.out_ld = out_ld; a.out_off = out_off;
+  a.cout = cout; a.flags = flags; a.aff_scale = aff_scale; a.aff_shift = aff_shift;
+  a.stats = stat_part;
+  a.border = border;
+  a.pool_out = pool_out; a.pool_ld = pool_ld; a.pool_idx = pool_idx; a.pool_sign = pool_sign;
+  CNN_REQUIRE(pool_out && pool_idx, "conv3x3_fwd_pool: missing pool buffers");
+  CNN_REQUIRE(!(flags & CNNITMO_STATS) || stat_part, "conv3x3_fwd_pool: STATS without buffer");
+  CNN_REQUIRE(!(flags & CNNITMO_AFFINE) || (aff_scale && aff_shift), "conv3x3_fwd_pool: AFFINE without coefficients");
+  const bool f32 = dtype == CNNITMO_F32;
+  if ((dtype != CNNITMO_BF16 && !f32) || !halo_handles(a, f32)) {
+    cnnitmo_set_error("conv3x3_fwd_pool: unsupported (halo kernel with an epilogue, even h/w, pool_ld >= cout)");
+    return CNNITMO_EUNSUPPORTED;
+  }
+  return launch_halo(a, (hipStream_t)stream, "conv3x3_fwd_pool", f32);
+}
+
+extern "C" int cnnitmo_conv3x3_pool_supported(int dtype, int n, int h, int w, int cin, int cout) {
+  FwdArgs a = base_args();
+  a.a = (const void*)16; a.a_ld = cin;
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cin; a.N = cout; a.M = (long)n * h * w; a.out_ld = cout; a.cout = cout;
+  a.flags = CNNITMO_RELU;
+  a.pool_out = (void*)16; a.pool_ld = cout; a.pool_idx = (unsigned char*)16;
+  const bool f32 = dtype == CNNITMO_F32;
+  if (dtype != CNNITMO_BF16 && !f32) return 0;
+  return halo_handles(a, f32) ? 1 : 0;
+}
+
 extern "C" int cnnitmo_conv3x3_fwd_cat(int dtype, const void* x1, int x1_ld, int x1_off, int c1, const void* x2,
                                        int x2_ld, int x2_off, int n, int h, int w, int cin, const void* wt,
                                        const float* bias, int cout, void* out, int out_ld, int out_off, int flags,

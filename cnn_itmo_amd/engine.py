@@ -68,6 +68,7 @@ class Value:
         self.cs = None  # coefficient buffers of the owner (persist across steps)
         self.ch = None
         self.split = False  # concat whose members keep dense buffers of their own (Engine._plan_split_concats)
+        self.coef_src = None  # a fused pool's output: folded with its input's BN coefficients
 
     def owner(self):
         return self.place[0] if self.place else self
@@ -105,6 +106,8 @@ class Value:
                 o.mark_grad()
 
     def ensure_coef(self, device):
+        if self.coef_src is not None:
+            return self.coef_src.ensure_coef(device)
         o = self.owner()
         if o.cs is None:
             o.cs = torch.ones(o.c, device=device, dtype=torch.float32)
@@ -112,6 +115,8 @@ class Value:
 
     def coef(self):
         """(scale, shift) [c] fp32 slices of the owner's coefficient buffers."""
+        if self.coef_src is not None:
+            return self.coef_src.coef()
         o = self.owner()
         off = self.place[1] if self.place else 0
         return o.cs[off:off + self.c], o.ch[off:off + self.c]
@@ -141,6 +146,7 @@ class Stage:
 class BlockStage(Stage):
     def __init__(self, kind, conv, relu, bn, drop, drop_id, vin, vout):
         self.kind, self.conv, self.relu, self.bn, self.drop = kind, conv, relu, bn, drop
+        self.pool = None  # the PoolStage whose 2x2 max-pool this conv's epilogue computes (Engine._plan_pool_fusion)
         self.drop_id = drop_id
         self.vin, self.vout = vin, vout
         self.cin = vin.c if kind != "c3in" else 3
@@ -211,6 +217,9 @@ class BlockStage(Stage):
                     a, b = self.vin.members
                     ops.conv3x3_fwd_cat(e.dt, a.view(n), b.view(n), self.w_fold, self.b_fold, out_view, flags, aff,
                                         stats, border=self.border)
+                elif self.pool is not None:
+                    ops.conv3x3_fwd_pool(e.dt, self.vin.view(n), self.w_fold, self.b_fold, out_view,
+                                         *self._pool_bufs(n), flags=flags, aff=aff, stats=stats, border=self.border)
                 else:
                     ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fold, self.b_fold, out_view, flags, aff,
                                     stats, border=self.border)
@@ -222,6 +231,9 @@ class BlockStage(Stage):
         if self.kind == "c3" and self.vin.split:
             a, b = self.vin.members
             ops.conv3x3_fwd_cat(e.dt, a.view(n), b.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
+        elif self.kind == "c3" and self.pool is not None:
+            ops.conv3x3_fwd_pool(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, *self._pool_bufs(n), flags=flags,
+                                 aff=aff, stats=stats)
         elif self.kind == "c3":
             ops.conv3x3_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
         elif self.kind == "c3in" and self.direct:
@@ -232,6 +244,17 @@ class BlockStage(Stage):
                              out_view, flags, aff, stats)
         else:
             ops.tconv_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
+
+    def _pool_bufs(self, n):
+        """(pooled output, window indices, pool sign) for the fused MaxPooling2D: in training
+        the epilogue stores r with the BN folded into the consumers, so it pools r by the
+        sign of gamma (= the sign of the BN scale); in inference it stores y and pools by the
+        maximum."""
+        e, pv = self.eng, self.pool.vout
+        pv.ensure(n, e.tdtype, e.device)
+        self.pool.idx = torch.empty(n * pv.h * pv.w * pv.c, dtype=torch.uint8, device=e.device)
+        sign = e.p(self.bn.name + "/gamma") if (e.training and self.vout.folded) else None
+        return pv.buf, self.pool.idx, sign
 
     def _gemm_rows(self, n):
         if self.kind == "t2":
@@ -542,10 +565,14 @@ class PoolStage(Stage):
     def __init__(self, layer, vin, vout):
         self.layer, self.vin, self.vout, self.name = layer, vin, vout, layer.name
 
+    fused = False  # the producer's epilogue pools (Engine._plan_pool_fusion)
+
     def forward(self, n, training):
         e = self.eng
         if self.vout.place:
             raise NotImplementedError("MaxPooling2D output feeding a concatenate")
+        if self.fused:
+            return  # written by the producer's conv3x3_fwd_pool (pooled value + window indices)
         self.vout.ensure(n, e.tdtype, e.device)
         self.idx = torch.empty(n * self.vout.h * self.vout.w * self.vout.c, dtype=torch.uint8, device=e.device)
         aff = self.vin.coef() if training and self.vin.folded else None
@@ -562,7 +589,11 @@ class PoolStage(Stage):
             pp = n * (v.h // 2) * (v.w // 2)
             rows = ops.bn_bwd_rows(pp, v.c)
             pm = torch.empty(rows * 2 * v.c, device=e.device, dtype=torch.float32)
-            ops.pool_bnsums(e.dt, self.vout.gbuf, self.idx, v.view(n), v.producer.smean, v.producer.sinv, pm)
+            if self.fused:  # the pooled value IS r at the window index
+                ops.pool_bnsums_pooled(e.dt, self.vout.gbuf, self.vout.buf, n, v.h, v.w, v.c, v.producer.smean,
+                                       v.producer.sinv, pm)
+            else:
+                ops.pool_bnsums(e.dt, self.vout.gbuf, self.idx, v.view(n), v.producer.smean, v.producer.sinv, pm)
             v.bn_contrib.append(pm)
             v.pool_route = (self.vout.gbuf, self.idx)
         else:
@@ -802,6 +833,7 @@ class Engine:
         self.device = torch.device(device)
         self.stages = compile_graph(model, fold=os.environ.get("CNNITMO_NO_FOLD", "0") != "1")
         self._plan_split_concats()
+        self._plan_pool_fusion()
         self.training = False
         self.h_valid = None
         self.update_moving = True
@@ -858,6 +890,33 @@ class Engine:
                     and ops.wgrad_cat_supported(1, v.h, v.w, c1, c, rs[0].cout)):
                 continue
             v.split = True
+
+    def _plan_pool_fusion(self):
+        """MaxPooling2D into its producer's epilogue (model.py:209-220: ConvBN -> pool at
+        levels 0-2): the conv3x3 whose BN output the pool reads writes the pooled value and
+        window indices itself (cnnitmo_conv3x3_fwd_pool), which removes the pool's re-read of
+        the full-resolution output.  In training the producer stores r (BN folded into its
+        consumers) and pools r by sign(gamma); the pooled value is then a folded value too,
+        with the producer's BN coefficients (Value.coef_src), and its consumer conv folds them
+        like any other.  Needs: a 'c3' producer with BN and no Dropout (Dropout outputs are
+        materialised by bn_apply), BN folding on, the halo kernel for the producer's sizes.
+        CNNITMO_POOL_FUSE=0: the stand-alone pool kernel."""
+        if os.environ.get("CNNITMO_POOL_FUSE", "1") == "0":
+            return
+        for st in self.stages:
+            if not isinstance(st, PoolStage):
+                continue
+            v = st.vin
+            prod = v.producer
+            if (prod is None or prod.kind != "c3" or prod.bn is None or prod.drop is not None or not v.folded
+                    or v.split or prod.vin.split or st.vout.place):
+                continue
+            if not ops.pool_supported(self.dt, 1, v.h, v.w, prod.vin.c if prod.kind == "c3" else 3, prod.cout):
+                continue
+            st.fused = True
+            prod.pool = st
+            st.vout.folded = True
+            st.vout.coef_src = v
 
     # ---- parameter access ---------------------------------------------------
     def _slice(self, flat, table, key):

@@ -66,6 +66,20 @@ def conv3x3_fwd(dt, x: View, wt, bias, out: View, flags=0, aff=None, stats=None,
          stream_ptr())
 
 
+def conv3x3_fwd_pool(dt, x: View, wt, bias, out: View, pool_out, pool_idx, pool_sign=None, flags=0, aff=None,
+                     stats=None, border=None):
+    """conv3x3_fwd + the output's 2x2 MaxPooling2D in the epilogue (cnnitmo_conv3x3_fwd_pool):
+    pool_out / pool_idx [n, h/2, w/2, cout] dense; pool_sign [cout] (None: max)."""
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_conv3x3_fwd_pool", dt, x.ptr, x.ld, x.off, x.n, x.h, x.w, x.c, ptr(wt), ptr(bias),
+         out.c, out.ptr, out.ld, out.off, flags, ptr(sc), ptr(sh), ptr(stats), ptr(border),
+         ptr(pool_out), out.c, ptr(pool_idx), ptr(pool_sign), stream_ptr())
+
+
+def pool_supported(dt, n, h, w, cin, cout):
+    return query("cnnitmo_conv3x3_pool_supported", dt, n, h, w, cin, cout) == 1
+
+
 def conv3x3_fwd_cat(dt, x1: View, x2: View, wt, bias, out: View, flags=0, aff=None, stats=None, border=None):
     """conv3x3_fwd over concatenate([x1, x2]) read from its members (cnnitmo_conv3x3_fwd_cat)."""
     sc, sh = aff if aff is not None else (None, None)
@@ -350,6 +364,13 @@ def pool_bnsums(dt, dyp, idx, r: View, mean, inv, part):
     bn_bwd_rows(pooled pixels, c)); r is the pool input's view."""
     call("cnnitmo_pool_bnsums", dt, ptr(dyp), ptr(idx), r.n, r.h, r.w, r.c, r.ptr, r.ld, r.off, ptr(mean),
          ptr(inv), ptr(part), stream_ptr())
+
+
+def pool_bnsums_pooled(dt, dyp, pr, n, h, w, c, mean, inv, part):
+    """pool_bnsums when the producer pooled in its epilogue: pr = r at each window index
+    [n, h/2, w/2, c] dense (h, w: the pool INPUT's size)."""
+    call("cnnitmo_pool_bnsums_pooled", dt, ptr(dyp), ptr(pr), n, h, w, c, ptr(mean), ptr(inv), ptr(part),
+         stream_ptr())
 
 
 def rmsprop(p, g, a, lr, rho, eps, grad_scale=1.0):

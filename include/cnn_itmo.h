@@ -75,6 +75,22 @@ int cnnitmo_conv3x3_fwd(int dtype, const void* x, int x_ld, int x_off, int n, in
                         const float* aff_shift, float* stat_part, const float* border,
                         void* stream);
 
+/* conv3x3_fwd with the 2x2 MaxPooling2D of its output fused into the epilogue
+ * (model.py:209-210, 214-215, 219-220: ConvBN -> MaxPooling2D).  pool_out
+ * [n, h/2, w/2] x pool_ld (dtype) gets the pooled stored value, pool_idx (same layout,
+ * bytes) its window index (first maximum in window order (0,0),(0,1),(1,0),(1,1), the
+ * cnnitmo_maxpool2x2_fwd rule).  pool_sign [cout] (nullable): per channel, pool by the
+ * maximum (> 0), the minimum (< 0) or take the first element (0) of the stored values:
+ * with the output stored as r and the BN folded into the consumers, sign(gamma) makes
+ * s * pooled + h the max-pool of y = r * s + h (s = gamma * invstd).  Requires even h, w
+ * and the halo kernel (cnnitmo_conv3x3_pool_supported). */
+int cnnitmo_conv3x3_fwd_pool(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w, int cin,
+                             const void* wt, const float* bias, int cout, void* out, int out_ld, int out_off,
+                             int flags, const float* aff_scale, const float* aff_shift, float* stat_part,
+                             const float* border, void* pool_out, int pool_ld, unsigned char* pool_idx,
+                             const float* pool_sign, void* stream);
+int cnnitmo_conv3x3_pool_supported(int dtype, int n, int h, int w, int cin, int cout);
+
 /* conv3x3_fwd over concatenate([x1, x2]) (model.py:261, Keras axis=3) read from its
  * two members, without a concat buffer: input channels [0, c1) are x1's view
  * (x1_ld, x1_off), channels [c1, cin) are x2's (x2_ld, x2_off).  bf16 only, c1 % 32 == 0,
@@ -343,6 +359,10 @@ int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* raw, int cou
 int cnnitmo_pool_bnsums(int dtype, const void* dyp, const uint8_t* idx, int n, int h, int w, int c,
                         const void* r, int r_ld, int r_off, const float* mean, const float* invstd,
                         float* part, void* stream);
+/* The same share when the pool was fused into the producer (cnnitmo_conv3x3_fwd_pool):
+ * pr [n, h/2, w/2, c] dense is r at each window's index, so no window is read. */
+int cnnitmo_pool_bnsums_pooled(int dtype, const void* dyp, const void* pr, int n, int h, int w, int c,
+                               const float* mean, const float* invstd, float* part, void* stream);
 /* Column sums of partial rows -> out[groups-folded c] (fp32, written). */
 int cnnitmo_colsum(const float* part, long rows, int cols, int groups, float* out,
                    void* workspace, void* stream);

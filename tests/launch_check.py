@@ -126,7 +126,7 @@ class _Acc:
 
 
 # every launching entry point of cnn_itmo_amd.ops (all of them go through ops.call)
-LAUNCHES = ("conv3x3_fwd", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
+LAUNCHES = ("conv3x3_fwd", "conv3x3_fwd_pool", "pool_bnsums_pooled", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
             "conv_wgrad", "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad", "conv1tap_fwd", "im2col_c3",
             "maxpool_fwd", "maxpool_bwd", "pool_bnsums", "bn_fwd_finalize", "bn_infer_coeffs", "bn_apply",
             "bn_bwd_reduce", "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3",
@@ -234,6 +234,12 @@ class LaunchChecker(ElementwiseChecks):
             tot = stats.view(-1, 2, cout).to(F64).sum(0)
             self._sums(lab + " stats", tot[0], s1, sa)
             self._sums(lab + " stats^2", tot[1], s2, sa2)
+
+    def _chk_conv3x3_fwd_pool(self, dt, x, wt, bias, out, pool_out, pool_idx, pool_sign=None, flags=0, aff=None,
+                              stats=None, border=None):
+        self._chk_conv3x3_fwd(dt, x, wt, bias, out, flags, aff, stats, border, tag="_pool")
+        self._chk_pool_of_stored(f"conv3x3_fwd_pool {x.n}x{x.h}x{x.w} {x.c}->{out.c}", dt, out, pool_out, pool_idx,
+                                 pool_sign)
 
     @staticmethod
     def _cat_view(x1, x2):

@@ -180,6 +180,39 @@ class ElementwiseChecks:
         tot = part.view(-1, 2, c).to(F64).sum(0)
         self._sums(lab, tot, s, sa)
 
+    def _chk_pool_of_stored(self, lab, dt, y, pool_out, pool_idx, pool_sign):
+        """The 2x2 pooling fused into a conv epilogue (cnnitmo_conv3x3_fwd_pool), bit-exact on
+        the STORED output y: per channel the first maximum of sign(pool_sign) * y in window
+        order (pool_sign None: of y; sign 0: the first element), the value stored there and
+        its window index."""
+        n, h, w, c = y.n, y.h, y.w, y.c
+        ho, wo = h // 2, w // 2
+        yt = y.tensor()
+        p4, i4 = pool_out.view(n, ho, wo, c), pool_idx.view(n, ho, wo, c)
+        m = torch.ones(c, dtype=F64, device=yt.device) if pool_sign is None else torch.sign(pool_sign.to(F64))
+        for i in range(n):
+            win = yt[i].to(F64).view(ho, 2, wo, 2, c).permute(0, 2, 1, 3, 4).reshape(ho, wo, 4, c)
+            key = win * m
+            first = (key == key.max(2).values.unsqueeze(2)).to(torch.uint8).argmax(2)
+            self._exact(lab + " pool idx", i4[i].long() == first)
+            self._exact(lab + " pool value", p4[i].to(F64) == win.gather(2, first.unsqueeze(2)).squeeze(2))
+
+    def _chk_pool_bnsums_pooled(self, dt, dyp, pr, n, h, w, c, mean, inv, part):
+        ho, wo = h // 2, w // 2
+        lab = f"pool_bnsums_pooled {n}x{h}x{w}x{c}"
+        d4, p4 = dyp.view(n, ho, wo, c), pr.view(n, ho, wo, c)
+        mu, iv = mean.to(F64), inv.to(F64)
+        s = torch.zeros(2, c, dtype=F64, device=part.device)
+        sa = torch.zeros_like(s)
+        for i in range(n):
+            g = d4[i].to(F64)
+            t = g * (p4[i].to(F64) - mu) * iv
+            s[0] += g.sum((0, 1))
+            s[1] += t.sum((0, 1))
+            sa[0] += g.abs().sum((0, 1))
+            sa[1] += t.abs().sum((0, 1))
+        self._sums(lab, part.view(-1, 2, c).to(F64).sum(0), s, sa)
+
     # ---- BatchNormalization forward -------------------------------------------------
     def _pre_bn_fwd_finalize(self, stats, rows, c, groups, count, gamma, beta, mmean, mvar, *a, **k):
         return None if mmean is None else (mmean.clone(), mvar.clone())

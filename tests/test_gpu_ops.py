@@ -415,3 +415,45 @@ def test_rmsprop():
     torch.cuda.synchronize()
     np.testing.assert_allclose(pt.cpu().numpy(), pr, atol=1e-6)
     np.testing.assert_allclose(at.cpu().numpy(), ar, atol=1e-6)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("cin,cout,H,W", [(32, 32, 16, 64), (64, 64, 18, 70), (128, 128, 8, 96), (64, 64, 6, 34)])
+def test_conv3x3_fwd_pool(dt, cin, cout, H, W):
+    """cnnitmo_conv3x3_fwd_pool: the conv output is the plain conv3x3_fwd's bit for bit,
+    and the pooled value / window index are the first-max rule applied to the STORED
+    output with the per-channel mode sign(pool_sign) (max, min, first) -- and plain max
+    without a sign (inference).  Partial tiles in both directions (W % 32, H % 16)."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin + H)
+    N = 2
+    x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
+    w = (rng.standard_normal((cout, 3, 3, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    d, T = DT[dt], TDT[dt]
+    if not ops.pool_supported(d, N, H, W, cin, cout):
+        pytest.skip("halo kernel does not take this shape")
+    wf = torch.empty(w.size, dtype=T, device="cuda")
+    ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cin, wf, None)
+    xv = ops.View(dev(x, dt).reshape(-1), N, H, W, cin, cin)
+    bias = torch.tensor(b).cuda()
+    ref = ops.new_view(N, H, W, cout, T)
+    rows = ops.conv3x3_stat_rows(d, N, H, W, cin, cout)
+    st0 = torch.zeros(rows * 2 * cout, device="cuda")
+    ops.conv3x3_fwd(d, xv, wf, bias, ref, 1 | 2, stats=st0)
+    sign = torch.tensor(np.resize([1.0, -0.5, 0.0, 3.0], cout).astype(np.float32)).cuda()
+    for sg in (sign, None):
+        out = ops.new_view(N, H, W, cout, T)
+        pv = torch.empty(N * (H // 2) * (W // 2) * cout, dtype=T, device="cuda")
+        pi = torch.empty(N * (H // 2) * (W // 2) * cout, dtype=torch.uint8, device="cuda")
+        st = torch.zeros(rows * 2 * cout, device="cuda")
+        ops.conv3x3_fwd_pool(d, xv, wf, bias, out, pv, pi, sg, flags=1 | 2, stats=st)
+        torch.cuda.synchronize()
+        assert torch.equal(out.buf, ref.buf)
+        assert torch.allclose(st.view(rows, 2, cout).sum(0), st0.view(rows, 2, cout).sum(0), rtol=1e-5, atol=1e-3)
+        y = ref.buf.view(N, H // 2, 2, W // 2, 2, cout).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4, cout)
+        m = torch.ones(cout, device="cuda") if sg is None else torch.sign(sg)
+        key = y.double() * m.double()
+        first = (key == key.max(3, keepdim=True).values).to(torch.uint8).argmax(3)
+        assert torch.equal(pi.view(N, H // 2, W // 2, cout), first.to(torch.uint8))
+        assert torch.equal(pv.view(N, H // 2, W // 2, cout), y.gather(3, first.unsqueeze(3)).squeeze(3))

@@ -346,3 +346,33 @@ def test_consumer_sums_check(mode):
     chk._chk_bn_consumer_sums(*args, part.view(-1))
     j = int((part.view(-1).abs() > 1e-3).nonzero()[0])
     _fails(chk._chk_bn_consumer_sums, *args, _bump(part.view(-1), j))
+
+
+@pytest.mark.parametrize("dt", [L.BF16, L.F32])
+def test_fused_pool_checks(dt):
+    """The fused-pool checks (cnnitmo_conv3x3_fwd_pool's pooled value and window index,
+    cnnitmo_pool_bnsums_pooled): an emulation of the contract passes, a wrong index, a
+    wrong value or a wrong sum fails.  Channel modes: max (+), min (-), first (0)."""
+    T = BF if dt == L.BF16 else F32
+    g = torch.Generator().manual_seed(3)
+    n, h, w, c = 2, 6, 8, 16
+    y = (torch.randint(0, 5, (n * h * w * c,), generator=g).float() / 4).to(T)  # many exact ties
+    yv = View(y, n, h, w, c, c)
+    sign = torch.tensor([1.0, -1.0, 0.0, 2.0] * 4)
+    win = y.view(n, h // 2, 2, w // 2, 2, c).permute(0, 1, 3, 2, 4, 5).reshape(n, h // 2, w // 2, 4, c).double()
+    key = win * torch.sign(sign).double()
+    first = (key == key.max(3, keepdim=True).values).to(torch.uint8).argmax(3)
+    pv = win.gather(3, first.unsqueeze(3)).squeeze(3).to(T).reshape(-1)
+    pi = first.to(torch.uint8).reshape(-1)
+    chk = _checker(dt)
+    chk._chk_pool_of_stored("pool", dt, yv, pv, pi, sign)
+    _fails(chk._chk_pool_of_stored, "pool", dt, yv, pv, (pi + 1) % 4, sign)
+    _fails(chk._chk_pool_of_stored, "pool", dt, yv, _bump(pv), pi, sign)
+    _fails(chk._chk_pool_of_stored, "pool", dt, yv, pv, pi, None)  # max everywhere: the min / first channels differ
+    # pooled BN sums
+    dyp = torch.randn(n * (h // 2) * (w // 2) * c, generator=g).to(T)
+    mean, inv = torch.rand(c, generator=g), torch.rand(c, generator=g) + 0.5
+    gd, pd = dyp.double().view(-1, c), pv.double().view(-1, c)
+    part = torch.stack([gd.sum(0), (gd * (pd - mean.double()) * inv.double()).sum(0)]).float()[None]
+    chk._chk_pool_bnsums_pooled(dt, dyp, pv, n, h, w, c, mean, inv, part)
+    _fails(chk._chk_pool_bnsums_pooled, dt, dyp, pv, n, h, w, c, mean, inv, _bump(part, i=c + 2, by=1.0))
