@@ -79,7 +79,11 @@ constexpr int PFT = 5;
 // small-K layers (cin <= 64: level 1 and 2) the per-item weight pieces were half of
 // every stage's DMA.
 constexpr int RCH = 2;
-template <int BN, bool RES> struct HCfg {
+// THT: tile rows (16; 8 for dec9a's forward: 96 input channels with all three weight chunks
+// resident, which needs the smaller patch to fit two stages beside them)
+template <int BN, bool RES, int THT = 16> struct HCfg {
+  static constexpr int RCH = THT == 8 ? 3 : ::RCH;
+  static constexpr int PPC = ((THT + 2) * PW + 15) / 16, NPI = (PPC + NWAVE - 1) / NWAVE;
   static constexpr int FN = BN / 16, FP = FN / 2;        // fragments / 32-column pairs
   static constexpr int BPC = KT * BN / 16;               // weight pieces
   static constexpr int NBI = (BPC + NWAVE - 1) / NWAVE;  // weight pieces per wave
@@ -92,7 +96,7 @@ template <int BN, bool RES> struct HCfg {
   static constexpr int PAR = SCR + 1024;    // [4][BN] fp32 epilogue parameters (bias, scale, shift, pool mode)
   static constexpr int UTB = PAR + 4 * BN * 4;  // [BN][8] fp32 border table
   static constexpr int SMEM = UTB + BN * 8 * 4;
-  static constexpr int NST = FM * FP;  // 16-byte stores per wave per epilogue
+  static constexpr int NST = (THT / NWAVE) * FMR * FP;  // 16-byte stores per wave per epilogue
   static_assert(SMEM <= 160 * 1024, "LDS");
   static_assert(BN % 32 == 0, "column pairs");
 };
@@ -123,9 +127,12 @@ struct HaloArgs {
 // and s * (min r) + h where gamma < 0: the kernel pools r by the per-channel mode sign(gamma)
 // (pool_sign), and the pooled value is itself a folded value.  Inference stores y (AFFINE)
 // and pools it by its maximum.
-template <typename TE, int BN, int EPI, bool RES, bool POOL = false>
+template <typename TE, int BN, int EPI, bool RES, bool POOL = false, int THT = 16>
 __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
-  using C = HCfg<BN, RES>;
+  using C = HCfg<BN, RES, THT>;
+  constexpr int TH = THT, RPW = TH / NWAVE, FM = RPW * FMR, PROWS = (TH + 2) * PW;  // (shadow the 16-row defaults)
+  constexpr int PPC = C::PPC, NPI = C::NPI;
+  static_assert(RPW >= 1, "a tile row per wave at least");
   constexpr int FN = C::FN, FP = C::FP, L = C::L, NBI = C::NBI, STAGE = C::STAGE, ST = C::ST;
   constexpr int ES = sizeof(TE), CC = 64 / ES, PE = 16 / ES;
   static_assert(!POOL || (EPI == 1 && RPW % 2 == 0), "pooling: the forward epilogue, whole window rows per wave");
@@ -784,7 +791,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 }
 
 struct HaloPlan {
-  int bn, epi;
+  int bn, epi, th;
   bool res;
 };
 
@@ -841,11 +848,30 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
     return e ? atoi(e) : 1;
   }();
   pl.res = res && a.cin <= (f32 ? 16 : 32) * RCH;
+  // dec9a's forward (cin 96 = the [conv1 32 | up9 64] concat, 64 output channels, one column
+  // block): 8-row tiles with all three weight chunks resident (2 x 22 KB patches + 108 KB
+  // weights) instead of 16-row tiles streaming 36 KB of weights per 32-channel item.
+  // CNNITMO_HALO_TH8=0: 16-row tiles
+  static const int th8 = [] {
+    const char* e = getenv("CNNITMO_HALO_TH8");
+    return e ? atoi(e) : 1;
+  }();
+  pl.th = 16;
+  if (th8 && !f32 && pl.epi == 1 && pl.bn == 64 && a.N == 64 && a.cin == 96 && !a.pool_out && res) {
+    pl.th = 8;
+    pl.res = true;
+  }
   return true;
 }
 
 template <typename T, int BN, int EPI>
-void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
+void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s, int th = 16) {
+  if constexpr (EPI == 1 && BN == 64 && sizeof(T) == 2) {
+    if (th == 8) {  // (halo_plan: resident weights, no pooling)
+      hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, false, 8>), dim3(grid), dim3(NT), 0, s, h);
+      return;
+    }
+  }
   if constexpr (EPI == 1) {
     if (h.f.pool_out) {
       if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
@@ -872,7 +898,7 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
   HaloArgs h;
   h.f = a;
   h.tiles_x = (a.wo + TW - 1) / TW;  // partial edge tiles are masked
-  h.tiles_y = (a.ho + TH - 1) / TH;
+  h.tiles_y = (a.ho + pl.th - 1) / pl.th;
   h.nchunks = a.cin / (f32 ? 16 : 32);
   h.tiles = (long)a.nimg * h.tiles_x * h.tiles_y;
   h.nblocks = a.N / pl.bn;
@@ -894,7 +920,7 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
     if (pl.bn == 64) launch_cfg<bf16, 64, 2>(h, pl.res, grid, s);
     else launch_cfg<bf16, 32, 2>(h, pl.res, grid, s);
   } else if (pl.epi == 1) {
-    if (pl.bn == 64) launch_cfg<bf16, 64, 1>(h, pl.res, grid, s);
+    if (pl.bn == 64) launch_cfg<bf16, 64, 1>(h, pl.res, grid, s, pl.th);
     else launch_cfg<bf16, 32, 1>(h, pl.res, grid, s);
   } else {
     if (pl.bn == 64) launch_cfg<bf16, 64, 0>(h, pl.res, grid, s);
@@ -907,7 +933,8 @@ const char* halo_name(const FwdArgs& a, bool f32) {
   HaloPlan pl;
   if (!halo_plan(a, pl, f32)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "halo_conv_kernel<%s%d,%d%s>", f32 ? "f32," : "", pl.bn, pl.epi, pl.res ? ",wres" : "");
+  snprintf(buf, sizeof(buf), "halo_conv_kernel<%s%d,%d%s%s>", f32 ? "f32," : "", pl.bn, pl.epi, pl.res ? ",wres" : "",
+           pl.th == 8 ? ",th8" : "");
   return buf;
 }
 

@@ -3,6 +3,8 @@ same seeded inputs.  fp32 path: max-abs <= 1e-4 relative to the output scale
 (MFMA f32 is an exact fp32 fma chain).  bf16 path: inputs are rounded to bf16
 first and the oracle sees the same rounded values; tolerance 1.5e-2 of scale
 (bf16 output rounding is 2^-8)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -457,3 +459,48 @@ def test_conv3x3_fwd_pool(dt, cin, cout, H, W):
         first = (key == key.max(3, keepdim=True).values).to(torch.uint8).argmax(3)
         assert torch.equal(pi.view(N, H // 2, W // 2, cout), first.to(torch.uint8))
         assert torch.equal(pv.view(N, H // 2, W // 2, cout), y.gather(3, first.unsqueeze(3)).squeeze(3))
+
+
+@pytest.mark.parametrize("H,W", [(16, 64), (20, 70), (8, 40)])
+@pytest.mark.parametrize("th8", ["1", "0"])
+def test_conv3x3_fwd_cat_dec9a(H, W, th8):
+    """cnnitmo_conv3x3_fwd_cat on dec9a's shape ([conv1 32 | up9 64] -> 64, model.py:261-262)
+    vs the oracle on the materialised concat: ReLU + BN sums, with the 8-row resident-weight
+    tiles (default) and with the 16-row streamed ones (CNNITMO_HALO_TH8=0, read once per
+    process: run in a subprocess)."""
+    import subprocess
+    import sys as _sys
+    code = f"""
+import sys, numpy as np, torch
+sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+from cnn_itmo_amd import ops
+from oracle import unet_ref as R
+rng = np.random.default_rng({H} + {W})
+N, H, W = 2, {H}, {W}
+x1 = rng.standard_normal((N, H, W, 32)).astype(np.float32)
+x2 = rng.standard_normal((N, H, W, 64)).astype(np.float32)
+w = (rng.standard_normal((64, 3, 3, 96)) * 0.1).astype(np.float32)
+b = rng.standard_normal(64).astype(np.float32)
+bf = lambda a: torch.tensor(a).to(torch.bfloat16)
+wf = torch.empty(w.size, dtype=torch.bfloat16, device="cuda")
+ops.prep_conv3x3(1, torch.tensor(w).cuda(), 64, 96, wf, None)
+v1 = ops.View(bf(x1).cuda().reshape(-1), N, H, W, 32, 32)
+v2 = ops.View(bf(x2).cuda().reshape(-1), N, H, W, 64, 64)
+out = ops.new_view(N, H, W, 64, torch.bfloat16)
+rows = ops.conv3x3_stat_rows(1, N, H, W, 96, 64)
+st = torch.zeros(rows * 128, device="cuda")
+ops.conv3x3_fwd_cat(1, v1, v2, wf, torch.tensor(b).cuda(), out, 1 | 2, stats=st)
+torch.cuda.synchronize()
+xc = np.concatenate([bf(x1).double().numpy(), bf(x2).double().numpy()], 3)
+ref = np.maximum(R.conv2d_same(xc, bf(w).double().numpy(), b), 0)
+got = out.buf.float().cpu().numpy().reshape(ref.shape)
+err = float(np.abs(got - ref).max()) / max(1.0, float(np.abs(ref).max()))
+s = st.view(rows, 2, 64).double().sum(0).cpu().numpy()
+serr = float(np.abs(s[0] - got.reshape(-1, 64).sum(0)).max()) / max(1.0, float(np.abs(got).sum()))
+print("kernel", ops.query("cnnitmo_conv3x3_kernel_name", 1, N, H, W, 96, 64, 0).decode(), "err", err, "serr", serr)
+assert err <= 1.5e-2 and serr <= 1e-5
+"""
+    env = dict(os.environ, CNNITMO_HALO_TH8=th8)
+    r = subprocess.run([_sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    print(r.stdout.strip().splitlines()[-1])
