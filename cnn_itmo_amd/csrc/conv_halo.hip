@@ -70,6 +70,11 @@ constexpr int PFT = 5;
 #endif
 // tap offset of the DMA issue window for waves NWAVE/2.. (the second wave on each SIMD):
 // the two waves of a SIMD then issue their pieces in different taps
+// EPI 2 (bf16): issue the epilogue's r loads during the tile's last tap (1) or after its
+// MFMAs (0)
+#ifndef HALO_RTAP
+#define HALO_RTAP 0
+#endif
 #ifndef HALO_PFT_OFF
 #define HALO_PFT_OFF 0
 #endif
@@ -101,6 +106,11 @@ template <int BN, bool RES, int THT = 16> struct HCfg {
   static_assert(BN % 32 == 0, "column pairs");
 };
 
+
+// row_ror:N within each 16-lane row (DPP)
+template <int N> __device__ __forceinline__ float dpp_ror(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x120 + N, 0xF, 0xF, false));
+}
 
 // store sink for EPI 2's out-of-image pixels (global stores, fixed count per wave)
 __device__ __attribute__((aligned(256))) uint4 h_sink[64];
@@ -138,7 +148,12 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   static_assert(!POOL || (EPI == 1 && RPW % 2 == 0), "pooling: the forward epilogue, whole window rows per wave");
   // stores per wave per epilogue (+ POOL: a value and an index store per window row and column block)
   constexpr int NST = C::NST * (ES == 4 ? 2 : 1) + (POOL ? FP * (RPW / 2) * FMR * (ES == 4 ? 3 : 2) : 0);
-  __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
+  // EPI 2 with HALO_RTAP: the dz parity sums live in per-wave LDS slots [NWAVE][4][BN] (over
+  // the border table, which EPI 2 does not use) instead of 32 registers
+  constexpr bool SLOT = HALO_RTAP && EPI == 2 && ES == 2;
+  constexpr int SMEM = SLOT ? C::UTB + NWAVE * 4 * BN * 4 : C::SMEM;
+  static_assert(SMEM <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the vmcnt switch
@@ -177,6 +192,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       const int k = i / BN, c = n0 + i % BN;
       par[i] = (c >= p.bnb_c0 && c < p.bnb_c1) ? p.bnb_coef[k * cbn + c - p.bnb_c0] : 0.f;
     }
+    if constexpr (SLOT)
+      for (int i = tid; i < NWAVE * 4 * BN; i += NT) utb[i] = 0.f;
   }
 
   // item position: (image, tile row, tile column, chunk); tile rows fastest
@@ -193,6 +210,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     ip.x0 = txi * TW;
     ip.ch = 0;
   }
+  Pos ep = ip;  // position of the item being computed (the ring below advances ip ahead of it)
   auto step = [&](Pos& s) {
     if (++s.ch < nch) return;
     s.ch = 0;
@@ -307,7 +325,19 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const bool ok = e.y0 + wave * RPW + rr < p.ho && e.x0 + col < p.wo && c >= p.bnb_c0 && c < p.bnb_c1;
     return ok ? (unsigned)((((long)rr * p.wo + col) * p.bnb_r_ld + (c - p.bnb_c0)) * ES) : OOB;
   };
-  auto compute = [&](int buf, bool pf, int ch) {
+  // EPI 2 (bf16, HALO_RTAP): r of the tile, loaded during the last item's last tap (whose
+  // next-tap fragment registers are free) instead of after its MFMAs
+  dma::i32x4 rvp[EPI == 2 && ES == 2 ? FM : 1][EPI == 2 && ES == 2 ? FP : 1];
+  auto load_r16 = [&](const Pos& e) {
+    if constexpr (EPI == 2 && ES == 2) {
+      const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int q = 0; q < FP; ++q) rvp[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r_off(e, f, q), 0, 0);
+    }
+  };
+  auto compute = [&](int buf, bool pf, int ch, const Pos* rl = nullptr) {
     const char* Ps = smem + buf * STAGE;
     const char* Bs = RES ? smem + C::WRES + ch * (C::BPC * 1024) : Ps + C::PATCH;
     uint4 af[2][FM], bfr[2][FN];
@@ -326,6 +356,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     for (int tap = 0; tap < KT; ++tap) {
       const int cur = tap & 1;
       if (tap + 1 < KT) load(tap + 1, cur ^ 1);
+      if (HALO_RTAP && tap == KT - 1 && rl) load_r16(*rl);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
@@ -342,7 +373,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   };
   // BN partial sums of the lane's pixels for its 8 channels of each pair (EPI 1), or
   // sums of dz by pixel-row parity (EPI 2; the lane's pixel-column parity is lane & 1)
-  constexpr int NSUM = EPI == 0 ? 1 : FP;
+  constexpr int NSUM = EPI == 0 || SLOT ? 1 : FP;
   float sa[NSUM][8], sb[NSUM][8];
 #pragma unroll
   for (int q = 0; q < NSUM; ++q)
@@ -519,16 +550,12 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // dz or g by column (global stores; out-of-image pixels go to the sink).  bf16: g is
   // rounded to bf16 first (as cnnitmo_bn_bwd_apply reads it from a bf16 buffer); fp32:
   // r of one column pair at a time (two 16-byte pieces per (pixel, 8 channels)).
-  auto epilogue_bnb16 = [&](const Pos& e) {
+  auto epilogue_bnb16 = [&](const Pos& e, bool pre) {
     const int oh0 = e.y0 + wave * RPW;
     const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
     const long m0 = ((long)e.img * p.ho + oh0) * p.wo + e.x0;  // the wave's first pixel
-    const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
-    dma::i32x4 rv[FM][FP];
-#pragma unroll
-    for (int f = 0; f < FM; ++f)
-#pragma unroll
-      for (int q = 0; q < FP; ++q) rv[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r_off(e, f, q), 0, 0);
+    if (!pre) load_r16(e);
+    auto& rv = rvp;
     // (also retires the next item's DMA, issued during this item's first taps).  Pulling
     // these pieces into L2 one item ahead by LDS-DMA into the sink measured 15-25 %
     // slower on every fused dgrad (dec6-dec8), whether issued before or after the
@@ -545,6 +572,11 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       lds8(par + cl, ca);
       lds8(par + BN + cl, cb);
       lds8(par + 2 * BN + cl, ce);
+      float ta[8], tb[8];  // SLOT: this tile's sums by pixel-row parity
+#pragma unroll
+      for (int k = 0; k < 8; ++k) ta[k] = tb[k] = 0.f;
+      float* sa_q = SLOT ? ta : sa[SLOT ? 0 : q];
+      float* sb_q = SLOT ? tb : sb[SLOT ? 0 : q];
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
@@ -558,8 +590,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           const float r = to_f32(rq[k]);
           if (fz) {
             v[k] = to_f32(from_f32<bf16>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f));
-            sa[q][k] += (ok && rr == 0) ? v[k] : 0.f;
-            sb[q][k] += (ok && rr == 1) ? v[k] : 0.f;
+            sa_q[k] += (ok && rr == 0) ? v[k] : 0.f;
+            sb_q[k] += (ok && rr == 1) ? v[k] : 0.f;
           } else {
             v[k] = gk;
           }
@@ -568,6 +600,30 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
                      : fz ? reinterpret_cast<uint4*>(Z + (size_t)m * cbn + (c - c0))
                           : reinterpret_cast<uint4*>(O + (size_t)m * p.out_ld + p.out_off + c);
         *dst = __builtin_bit_cast(uint4, pack8(v));
+      }
+      if constexpr (SLOT) {
+        if (fz) {  // (uniform per 16-lane row: g)
+          // sum over the row's lanes of equal pixel-column parity: rotate-adds by 2, 4, 8
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            ta[k] += dpp_ror<2>(ta[k]);
+            tb[k] += dpp_ror<2>(tb[k]);
+            ta[k] += dpp_ror<4>(ta[k]);
+            tb[k] += dpp_ror<4>(tb[k]);
+            ta[k] += dpp_ror<8>(ta[k]);
+            tb[k] += dpp_ror<8>(tb[k]);
+          }
+          if (pxl < 2) {  // slot [wave][row parity * 2 + column parity][BN]
+            float* sl = utb + (wave * 4 + pxl) * BN + cl;
+            float4* s0 = reinterpret_cast<float4*>(sl);
+            float4* s1 = reinterpret_cast<float4*>(sl + 2 * BN);
+            const float4 a0 = s0[0], a1 = s0[1], b0 = s1[0], b1 = s1[1];
+            s0[0] = float4{a0.x + ta[0], a0.y + ta[1], a0.z + ta[2], a0.w + ta[3]};
+            s0[1] = float4{a1.x + ta[4], a1.y + ta[5], a1.z + ta[6], a1.w + ta[7]};
+            s1[0] = float4{b0.x + tb[0], b0.y + tb[1], b0.z + tb[2], b0.w + tb[3]};
+            s1[1] = float4{b1.x + tb[4], b1.y + tb[5], b1.z + tb[6], b1.w + tb[7]};
+          }
+        }
       }
     }
     zero_acc();
@@ -655,8 +711,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     zero_acc();
   };
 
-  auto epilogue_bnb = [&](const Pos& e) {
-    if constexpr (ES == 2) epilogue_bnb16(e);
+  auto epilogue_bnb = [&](const Pos& e, bool pre) {
+    if constexpr (ES == 2) epilogue_bnb16(e, pre);
     else epilogue_bnb32(e);
   };
 
@@ -674,7 +730,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     __syncthreads();
   }
   // ST-stage ring over items (see the file comment for the vmcnt accounting)
-  Pos ep = ip;  // position of the item being computed
   int issued = 0;
   int mq[ST];  // mq[k]: value of `issued` right after the loads of item t+k
 #pragma unroll
@@ -699,8 +754,15 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const bool pf = t + ST - 1 < T;
     if (pf) issue_prep(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
     const bool act = ep.y0 + wave * RPW < p.ho;
+    const bool rl = HALO_RTAP && EPI == 2 && ES == 2 && act && ep.ch == nch - 1;
+    if constexpr (HALO_RTAP && EPI == 2 && ES == 2) {  // no value carried between items
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int q = 0; q < FP; ++q) rvp[f][q] = __builtin_nondeterministic_value(rvp[f][q]);
+    }
     if (act) {
-      compute(buf, pf, ep.ch);  // issues those loads between its taps
+      compute(buf, pf, ep.ch, rl ? &ep : nullptr);  // issues those loads between its taps
     } else if (pf) {     // the wave's rows are all below the frame: no MFMAs, DMA share only
 #pragma unroll
       for (int q = 0; q < L; ++q) issue_piece(q);
@@ -711,7 +773,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       mq[ST - 1] = issued;
     }
     if (ep.ch == nch - 1) {
-      if constexpr (EPI == 2) epilogue_bnb(ep);
+      if constexpr (EPI == 2) epilogue_bnb(ep, rl);
       else epilogue(ep);
       issued += NST;
     }
@@ -743,6 +805,31 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
             st[32 * q + 8 * g + k] = sa[q][k];
             st[p.N + 32 * q + 8 * g + k] = sb[q][k];
           }
+      }
+    }
+  } else if constexpr (SLOT) {
+    const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
+    if (pxl < 2) {
+      const int cp = pxl;  // pixel-column parity
+      const float* sl = utb + wave * 4 * BN;
+#pragma unroll
+      for (int q = 0; q < FP; ++q) {
+        const int cl = 32 * q + 8 * g, c = n0 + cl;
+        if (c >= c0 && c < c1) {
+          if (p.bnb_par) {
+            float* st = p.stats + (size_t)row * 4 * cbn + (c - c0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              st[(size_t)(0 * 2 + cp) * cbn + k] = sl[(0 * 2 + cp) * BN + cl + k];
+              st[(size_t)(1 * 2 + cp) * cbn + k] = sl[(1 * 2 + cp) * BN + cl + k];
+            }
+          } else if (cp == 0) {
+            float* st = p.stats + (size_t)row * cbn + (c - c0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              st[k] = (sl[cl + k] + sl[2 * BN + cl + k]) + (sl[BN + cl + k] + sl[3 * BN + cl + k]);
+          }
+        }
       }
     }
   } else if constexpr (EPI == 2) {
