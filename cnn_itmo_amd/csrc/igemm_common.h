@@ -141,7 +141,7 @@ int launch_tconv_stream(int mode, const void* a, long a_ld, int a_off, const voi
 // weight-stationary GEMM, barrier-free after the prologue (bf16; up6..up8)
 // (f32: the fp32 inference forward, no BN sums)
 bool tconv_ws_handles(int mode, int cin, int cout, bool f32 = false);
-long tconv_ws_rows(int cin, int cout);
+long tconv_ws_rows(int cin, int cout, bool f32 = false);
 const char* tconv_ws_name(int mode, int cin, int cout, bool f32 = false);
 int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b, int n, int h, int w, int cin,
                     int cout, void* out, long out_ld, int out_off, const float* bias, int flags,

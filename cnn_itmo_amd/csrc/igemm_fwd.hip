@@ -342,6 +342,7 @@ extern "C" long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int c
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false))
     return tconv_stream_rows(0, n, h, w, cin, cout, false);
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout)) return tconv_ws_rows(cin, cout);
+  if (dtype == CNNITMO_F32 && tconv_ws_handles(0, cin, cout, true)) return tconv_ws_rows(cin, cout, true);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
   a.cin = cin; a.N = 4 * cout; a.a_ld = cin; a.out_ld = cout; a.M = (long)n * h * w;
@@ -484,7 +485,7 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
     return tconv_stream_name(dgrad ? 1 : 0, h, w, cin, cout, false);
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout))
     return tconv_ws_name(dgrad ? 1 : 0, cin, cout);
-  if (dtype == CNNITMO_F32 && !dgrad && tconv_ws_handles(0, cin, cout, true))  // (inference: no BN sums)
+  if (dtype == CNNITMO_F32 && !dgrad && tconv_ws_handles(0, cin, cout, true))
     return tconv_ws_name(0, cin, cout, true);
   if (dtype == CNNITMO_BF16 && dgrad && tconv_kc_handles(cin, cout)) return tconv_kc_name(cin, cout);
   FwdArgs a = base_args();
@@ -604,9 +605,9 @@ extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int 
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout))
     return launch_tconv_ws(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
                            aff_shift, stat_part, (hipStream_t)stream, "tconv2x2_fwd");
-  if (dtype == CNNITMO_F32 && !(flags & CNNITMO_STATS) && tconv_ws_handles(0, cin, cout, true))
+  if (dtype == CNNITMO_F32 && tconv_ws_handles(0, cin, cout, true))
     return launch_tconv_ws(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
-                           aff_shift, nullptr, (hipStream_t)stream, "tconv2x2_fwd", true);
+                           aff_shift, stat_part, (hipStream_t)stream, "tconv2x2_fwd", true);
   return dispatch(dtype, a, stream, "tconv2x2_fwd");
 }
 

@@ -70,14 +70,14 @@ __device__ __forceinline__ float row16_sum(float v) {
 // FM: 16-pixel fragment rows per wave tile (tile = 16 * FM pixels).  SQ: distinct BN-stat
 // column pairs of the block (BN / 32, or half that when the block spans two taps of the
 // same channels: BN = 2 * cout, whose pair q and q + SQ hold one channel's sums).
-// TE = float: the fp32 inference forward (MODE 0 without BN sums).  A 16-byte fragment
+// TE = float: the fp32 forward (MODE 0; BN sums in fp32 training).  A 16-byte fragment
 // piece is KE = 8 bf16 / 4 fp32 channels, so one K-step (four lane groups) is KS = 32 / 16
 // channels and 64 bytes in either type; Mma<float> runs a fragment as four 16x16x4 MFMAs.
 template <int MODE, int BN, int NKS, int FM = 2, int SQ = BN / 32, typename TE = bf16>
 __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   constexpr int FN = BN / 16, TP = 16 * FM;
   constexpr int ES = sizeof(TE), KE = 16 / ES, KS = 64 / ES;
-  static_assert(ES == 2 || MODE == 0, "fp32: the forward only");
+  static_assert(ES == 2 || MODE == 0, "fp32: the forward only (inference, or training with BN sums)");
   const TE* __restrict__ PA = (const TE*)p.a;
   const TE* __restrict__ PB = (const TE*)p.b;
   TE* __restrict__ PO = (TE*)p.out;
@@ -389,9 +389,9 @@ bool tconv_ws_handles(int mode, int cin, int cout, bool f32) {
 }
 
 // BN partial-sum rows of the forward: one per (pixel group, wave)
-long tconv_ws_rows(int cin, int cout) {
+long tconv_ws_rows(int cin, int cout, bool f32) {
   WSPlan pl;
-  if (!ws_plan(0, cin, cout, pl)) return 0;
+  if (!ws_plan(0, cin, cout, pl, f32)) return 0;
   return 8L * pl.gpx * NW;
 }
 
@@ -409,7 +409,6 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
                     bool f32) {
   WSPlan pl;
   CNN_REQUIRE(ws_plan(mode, cin, cout, pl, f32), "%s: no weight-stationary plan", what);
-  CNN_REQUIRE(!f32 || !(flags & CNNITMO_STATS), "%s: fp32 weight-stationary forward has no BN sums", what);
   CNN_REQUIRE(a_ld % 8 == 0 && a_off % 8 == 0 && out_ld % 4 == 0 && out_off % 4 == 0, "%s: misaligned views", what);
   CNN_REQUIRE((long)n * h * w < (1L << 31), "%s: too many pixels", what);
   CNN_REQUIRE(!(flags & CNNITMO_STATS) || (stats && mode == 0), "%s: STATS without buffer", what);
