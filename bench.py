@@ -194,9 +194,10 @@ class KernelTimer:
             return self._bracket("conv_c3_fwd_kernel" + ("<f32>" if dt == 0 else ""), fl, "c3 fwd", o["conv_c3_fwd"],
                                  dt, x, n, hv, h, w, *a, **k)
 
-        def conv_c3_wgrad(x, n, hv, h, w, *a, **k):
+        def conv_c3_wgrad(dt, x, n, hv, h, w, *a, **k):
             fl = 2.0 * n * h * w * 32 * 27
-            return self._bracket("conv_c3_wgrad_kernel + fold", fl, "c3 wgrad", o["conv_c3_wgrad"], x, n, hv, h, w, *a, **k)
+            kn = "conv_c3_wgrad_f32_kernel + fold" if dt == 0 else "conv_c3_wgrad_kernel + fold"
+            return self._bracket(kn, fl, "c3 wgrad", o["conv_c3_wgrad"], dt, x, n, hv, h, w, *a, **k)
 
         def wname(dt, ntaps, n, h, w, cin, cout):
             k = query("cnnitmo_wgrad_kernel_name", dt, ntaps, n, h, w, cin, cout).decode()

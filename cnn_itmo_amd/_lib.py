@@ -67,7 +67,7 @@ SIGNATURES = {
     "cnnitmo_head_fwd_bwd_g3": (i32, [i32, vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, f64, vp]),
     "cnnitmo_conv_c3_fwd": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_conv_c3_wgrad_workspace_bytes": (sz, [i32, i32, i32]),
-    "cnnitmo_conv_c3_wgrad": (i32, [vp, i32, i32, i32, i32, vp, vp, vp, sz, vp]),
+    "cnnitmo_conv_c3_wgrad": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, vp, sz, vp]),
     "cnnitmo_conv1tap_fwd": (i32, [i32, vp, i32, i64, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_tconv2x2_fwd": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_tconv2x2_dgrad": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, vp]),

@@ -24,7 +24,8 @@
 //                         flight under the current one; persistent grid, one fp32
 //                         slab per workgroup, fixed-order fold.
 //
-// HBM-bound: fwd 12 B read + 64 B written per pixel (+ stats), wgrad 12 + 64 B read.
+// HBM-bound: fwd 12 B read + 64 B written per pixel (+ stats), wgrad 12 + 64 B read
+// (fp32: 128 B written / read per pixel instead of 64).
 //
 // The forward also runs in fp32 (TO = float, the fp32 inference path of predict.py:62):
 // the same per-lane operand (8 k-values gathered from the fp32 image) goes to the MFMA
@@ -387,6 +388,125 @@ __global__ __launch_bounds__(256) void conv_c3_wgrad_kernel(const float* __restr
     slabs[(size_t)blockIdx.x * 1024 + e] = (part[e] + part[1024 + e]) + (part[2048 + e] + part[3072 + e]);
 }
 
+// fp32 weight gradient (fp32 training, main.py:126-132): the same persistent unit walk with
+// dz as [pixel][32] fp32 rows (128 B) and 16x16x4 f32 MFMAs.  The reduction axis is the
+// pixel: with Mma<float>'s k order a lane group g holds 4 consecutive pixels 4g..4g+3 of a
+// 16-pixel fragment, so the dz operand is 4 scalar LDS reads per lane (row = pixel, column =
+// channel; no transposed read exists for 32-bit elements) and the image-column operand 4
+// scalar reads as in the bf16 kernel.  84 KB of LDS (two 42 KB buffers): one workgroup per CU.
+constexpr int FDP = SEG * 8;                // fp32 dz pieces per unit (16 B = 4 channels)
+constexpr int FNI = FDP / 64 + WXI;         // DMA instructions per unit (42)
+constexpr int FBUF = FDP * 16 + WXI * 1024; // bytes per LDS buffer
+constexpr int FG_GRID = 256;                // persistent workgroups (one per CU)
+
+__global__ __launch_bounds__(256) void conv_c3_wgrad_f32_kernel(const float* __restrict__ x, int n, int hv, int h,
+                                                                int w, int segs, const float* __restrict__ dz,
+                                                                long units, float* __restrict__ slabs) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * FBUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const long G = gridDim.x;
+  const int w3 = w * 3;
+  (void)n;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int kof[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = 16 * j + li;
+    kof[j] = k < 27 ? (k / 9) * XRW + ((k % 9) / 3) * 3 + k % 3 : 0;
+  }
+  struct Unit {
+    int img, oh, w0;
+  };
+  auto unit = [&](long u) {
+    const long row = u / segs;
+    return Unit{(int)(row / h), (int)(row % h), (int)(u % segs) * SEG};
+  };
+  auto issue = [&](const Unit& un, int buf) {
+    char* B = lds + buf * FBUF;
+    const dma::i32x4 zs = dma::rsrc((uintptr_t)(dz + ((size_t)un.img * h + un.oh) * w * 32));
+    const dma::i32x4 xr = dma::rsrc((uintptr_t)(x + (size_t)un.img * hv * w3));
+    const long f00 = (long)(un.w0 - 4) * 3;
+#pragma unroll
+    for (int q = 0; q < (FNI + 3) / 4; ++q) {
+      const int T = wave + 4 * q;
+      if (T < FDP / 64) {  // dz: LDS row = pixel (8 pieces of 4 channels), natural order
+        const int pc = T * 64 + lane, row = pc >> 3;
+        const bool ok = un.w0 + row < w;
+        dma::lds16(ok ? (unsigned)(((un.w0 + row) * 32 + (pc & 7) * 4) * 4) : dma::OOB, zs, B + T * 1024);
+      } else if (T < FNI) {  // image rows oh-1 .. oh+1
+        const int t = T - FDP / 64, i = t * 64 + lane;
+        const int r = i / XPC, pc = i - (i / XPC) * XPC;
+        const int hh = un.oh - 1 + r;
+        const long f0 = f00 + pc * 4;
+        const bool ok = i < WXP && hh >= 0 && hh < hv && f0 >= 0 && f0 + 4 <= w3;  // (edge piece: patched)
+        dma::lds16(ok ? (unsigned)(((long)hh * w3 + f0) * 4) : dma::OOB, xr, B + FDP * 16 + t * 1024);
+      }
+    }
+  };
+  const int nis = (FNI - wave + 3) / 4;
+  long u = blockIdx.x;
+  int buf = 0;
+  if (u < units) issue(unit(u), 0);
+  for (; u < units; u += G) {
+    const Unit un = unit(u);
+    const int npx = min(SEG, w - un.w0);
+    __syncthreads();
+    const bool more = u + G < units;
+    if (more) issue(unit(u + G), buf ^ 1);
+    dma::wait_vm_dyn(more ? nis : 0);
+    __syncthreads();
+    const float* D = reinterpret_cast<const float*>(lds + buf * FBUF);
+    const float* X = D + FDP * 4;
+    if (w3 & 3) {  // the piece straddling the right frame edge: its nv valid floats by guarded loads
+      const int nv = w3 & 3, e0 = w3 - nv - (un.w0 - 4) * 3;
+      if (e0 < XRW && tid < 3 * 4) {
+        const int r = tid >> 2, k = tid & 3, hh = un.oh - 1 + r;
+        const bool ok = k < nv && hh >= 0 && hh < hv;
+        const_cast<float*>(X)[r * XRW + e0 + k] = ok ? x[((size_t)un.img * hv + hh) * w3 + (w3 - nv) + k] : 0.f;
+      }
+      __syncthreads();
+    }
+    if (wave * 64 < npx) {
+#pragma unroll
+      for (int fr = 0; fr < 4; ++fr) {
+        const int p0 = wave * 64 + fr * 16 + 4 * g;  // the lane's first pixel of the fragment
+        float a[2][4], b[2][4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) a[i][s] = D[(p0 + s) * 32 + 16 * i + li];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) b[j][s] = X[kof[j] + (p0 + s + 3) * 3];  // (+3: w0-4 origin, s=0 at -1)
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+      }
+    }
+    buf ^= 1;
+  }
+  __syncthreads();
+  float* part = reinterpret_cast<float*>(lds);
+  const int fk = lane >> 4, frow = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[wave * 1024 + (i * 16 + fk * 4 + r) * 32 + j * 16 + frow] = acc[i][j][r];
+  __syncthreads();
+  for (int e = tid; e < 1024; e += 256)
+    slabs[(size_t)blockIdx.x * 1024 + e] = (part[e] + part[1024 + e]) + (part[2048 + e] + part[3072 + e]);
+}
+
 // dw[co][k] (k < 27) = sum over the slabs: one workgroup per output channel, 8
 // slab ranges per column summed in order, then folded in a fixed order
 __global__ __launch_bounds__(256) void conv_c3_wgrad_fold_kernel(const float* __restrict__ slabs, int nslab,
@@ -449,21 +569,26 @@ extern "C" int cnnitmo_conv_c3_fwd(int dtype, const float* x, int n, int h_valid
 
 extern "C" size_t cnnitmo_conv_c3_wgrad_workspace_bytes(int n, int h, int w) {
   (void)n; (void)h; (void)w;
-  return (size_t)WG_GRID * 1024 * sizeof(float);
+  return (size_t)std::max(WG_GRID, FG_GRID) * 1024 * sizeof(float);
 }
 
-extern "C" int cnnitmo_conv_c3_wgrad(const float* x, int n, int h_valid, int h, int w, const void* dz, float* dw,
-                                     void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int cnnitmo_conv_c3_wgrad(int dtype, const float* x, int n, int h_valid, int h, int w, const void* dz,
+                                     float* dw, void* workspace, size_t ws_bytes, void* stream) {
+  CNN_REQUIRE(dtype == CNNITMO_BF16 || dtype == CNNITMO_F32, "conv_c3_wgrad: unsupported dtype %d", dtype);
   CNN_REQUIRE(x && dz && dw && workspace, "conv_c3_wgrad: null pointer");
   CNN_REQUIRE(n > 0 && h > 0 && w > 0 && h_valid >= 0 && h_valid <= h, "conv_c3_wgrad: bad shape");
   CNN_REQUIRE(ws_bytes >= cnnitmo_conv_c3_wgrad_workspace_bytes(n, h, w), "conv_c3_wgrad: workspace too small");
   const int segs = (w + SEG - 1) / SEG;
   const long units = (long)n * h * segs;
   CNN_REQUIRE((long)h_valid * w * 3 < (1L << 29) && (long)w * 64 < (1L << 31), "conv_c3_wgrad: frame too large");
-  const int blocks = (int)std::min<long>(units, WG_GRID);
+  const int blocks = (int)std::min<long>(units, dtype == CNNITMO_F32 ? FG_GRID : WG_GRID);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(conv_c3_wgrad_kernel, dim3(blocks), dim3(256), 0, s, x, n, h_valid, h, w, segs,
-                     (const bf16*)dz, units, (float*)workspace);
+  if (dtype == CNNITMO_F32)
+    hipLaunchKernelGGL(conv_c3_wgrad_f32_kernel, dim3(blocks), dim3(256), 0, s, x, n, h_valid, h, w, segs,
+                       (const float*)dz, units, (float*)workspace);
+  else
+    hipLaunchKernelGGL(conv_c3_wgrad_kernel, dim3(blocks), dim3(256), 0, s, x, n, h_valid, h, w, segs,
+                       (const bf16*)dz, units, (float*)workspace);
   hipLaunchKernelGGL(conv_c3_wgrad_fold_kernel, dim3(32), dim3(256), 0, s, (const float*)workspace, blocks, dw);
   return cnnitmo_check_launch("conv_c3_wgrad");
 }

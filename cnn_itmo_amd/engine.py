@@ -183,7 +183,7 @@ class BlockStage(Stage):
         # bf16 always (conv_c3 forward and weight gradient); fp32 for inference forwards
         # (the fp32 weight gradient still reads im2col columns, so fp32 training packs them)
         self.direct_ok = (self.kind == "c3in" and cout == 32 and os.environ.get("CNNITMO_C3_DIRECT", "1") != "0")
-        self.direct = self.direct_ok and eng.dt == L.BF16
+        self.direct = self.direct_ok
         if self.foldable:  # per-step folded copies (training)
             f32 = torch.float32
             self.w_fold = torch.empty_like(self.w_fwd)
@@ -277,7 +277,7 @@ class BlockStage(Stage):
         cout = self.cout
         P = n * self.vout.h * self.vout.w
         self.fold_active = training and self.foldable
-        self.direct = self.direct_ok and (e.dt == L.BF16 or not training)
+        self.direct = self.direct_ok
         if self.kind == "c3in" and not self.direct:
             self.cols = torch.empty(P * 32, dtype=e.tdtype, device=e.device)
             ops.im2col_c3(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.cols)
@@ -469,7 +469,7 @@ class BlockStage(Stage):
         with ctx:
             raw = torch.empty_like(dw) if targets else None
             if self.kind == "c3in" and self.direct:
-                ops.conv_c3_wgrad(e.x_in, n, e.h_valid, self.vout.h, self.vout.w, dz, dw)
+                ops.conv_c3_wgrad(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, dz, dw)
             elif self.kind == "c3in":
                 ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
                                dw, dw_cols=27)

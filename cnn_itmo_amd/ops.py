@@ -176,9 +176,9 @@ def conv_c3_fwd(dt, x, n, h_valid, h, w, wt, bias, out: View, flags=0, aff=None,
          ptr(sc), ptr(sh), ptr(stats), stream_ptr())
 
 
-def conv_c3_wgrad(x, n, h_valid, h, w, dz, dw):
+def conv_c3_wgrad(dt, x, n, h_valid, h, w, dz, dw):
     ws = workspace(query("cnnitmo_conv_c3_wgrad_workspace_bytes", n, h, w), dz.device)
-    call("cnnitmo_conv_c3_wgrad", ptr(x), n, h_valid, h, w, ptr(dz), ptr(dw), ws.data_ptr(), ws.numel(),
+    call("cnnitmo_conv_c3_wgrad", dt, ptr(x), n, h_valid, h, w, ptr(dz), ptr(dw), ws.data_ptr(), ws.numel(),
          stream_ptr())
 
 

@@ -202,10 +202,11 @@ int cnnitmo_conv_c3_fwd(int dtype, const float* x, int n, int h_valid, int h, in
                         const float* bias, void* out, int out_ld, int out_off, int flags,
                         const float* aff_scale, const float* aff_shift, float* stat_part, void* stream);
 /* dw [32][27] fp32 (OVERWRITTEN; OHWI) = sum_p dz[p][co] * patch(x, p)[k], dz [n*h*w][32]
- * bf16 contiguous.  Replaces cnnitmo_conv_wgrad(ntaps = 1) over im2col columns. */
+ * in dtype (bf16 or fp32) contiguous.  Replaces cnnitmo_conv_wgrad(ntaps = 1) over im2col
+ * columns. */
 size_t cnnitmo_conv_c3_wgrad_workspace_bytes(int n, int h, int w);
-int cnnitmo_conv_c3_wgrad(const float* x, int n, int h_valid, int h, int w, const void* dz, float* dw,
-                          void* workspace, size_t ws_bytes, void* stream);
+int cnnitmo_conv_c3_wgrad(int dtype, const float* x, int n, int h_valid, int h, int w, const void* dz,
+                          float* dw, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Conv2DTranspose(f, 2, strides=2, 'valid') -- replaces model.py:200

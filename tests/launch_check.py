@@ -360,8 +360,8 @@ class LaunchChecker(ElementwiseChecks):
             tot = stats.view(-1, 2, 32).to(F64).sum(0)
             self._sums(lab + " stats", tot[0], s1, sa)
 
-    def _chk_conv_c3_wgrad(self, x, n, hv, h, w, dz, dw):
-        xin = self._c3_input(x, n, hv, h, w, L.BF16)
+    def _chk_conv_c3_wgrad(self, dt, x, n, hv, h, w, dz, dw):
+        xin = self._c3_input(x, n, hv, h, w, dt)
         d4 = dz.view(n, h, w, 32)
         ref = torch.zeros(32, 3, 3, 3, dtype=F64, device=dz.device)
         for i in range(n):

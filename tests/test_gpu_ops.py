@@ -263,14 +263,12 @@ def test_first_layer_direct(N, Hv, H, W, ld, off, dt):
     st = stats.cpu().numpy().reshape(rows, 2, 32).sum(0)
     np.testing.assert_allclose(st[0], ref.reshape(-1, 32).sum(0), rtol=2e-2, atol=2e-2 * ref.size / 32)
     np.testing.assert_allclose(st[1], (ref ** 2).reshape(-1, 32).sum(0), rtol=3e-2)
-    if dt == "f32":
-        return
     dz = rng.standard_normal((N, H, W, 32)).astype(np.float32)
-    _, dw_ref, _ = R.conv2d_same_bwd(xp, rnd(w, "bf16"), rnd(dz, "bf16"), need_dx=False)
+    _, dw_ref, _ = R.conv2d_same_bwd(xp, rnd(w, dt), rnd(dz, dt), need_dx=False)
     dw = torch.empty(32, 27, device="cuda")
-    ops.conv_c3_wgrad(xd, N, Hv, H, W, dev(dz, "bf16"), dw)
+    ops.conv_c3_wgrad(DT[dt], xd, N, Hv, H, W, dev(dz, dt), dw)
     torch.cuda.synchronize()
-    close(host(dw).reshape(dw_ref.shape), dw_ref, "bf16", "first layer direct wgrad")
+    close(host(dw).reshape(dw_ref.shape), dw_ref, dt, "first layer direct wgrad")
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])

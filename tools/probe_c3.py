@@ -25,7 +25,7 @@ def main():
     out = ops.View(torch.zeros(n * h * w * a.ld, dtype=torch.bfloat16, device="cuda"), n, h, w, 32, a.ld, 0)
     rows = ops.query("cnnitmo_conv_c3_stat_rows", n, h, w)
     st = torch.zeros(rows * 64, device="cuda")
-    f = lambda: ops.conv_c3_fwd(x, n, hv, h, w, wt, bias, out, L.RELU | L.STATS, None, st)  # noqa: E731
+    f = lambda: ops.conv_c3_fwd(L.BF16, x, n, hv, h, w, wt, bias, out, L.RELU | L.STATS, None, st)  # noqa: E731
     f()
     ts = []
     for _ in range(10):
@@ -42,7 +42,7 @@ def main():
           f"sum(out) {float(y.double().sum()):.6e}  sum(stats) {float(st.view(rows, 2, 32).double().sum(0).sum()):.6e}")
     dz = (torch.randn(n * h * w * 32, generator=g, device="cuda") * 0.1).to(torch.bfloat16)
     dw = torch.empty(32 * 27, device="cuda")
-    fw = lambda: ops.conv_c3_wgrad(x, n, hv, h, w, dz, dw)  # noqa: E731
+    fw = lambda: ops.conv_c3_wgrad(L.BF16, x, n, hv, h, w, dz, dw)  # noqa: E731
     fw()
     ts = []
     for _ in range(10):
