@@ -485,8 +485,8 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
     return tconv_stream_name(dgrad ? 1 : 0, h, w, cin, cout, false);
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout))
     return tconv_ws_name(dgrad ? 1 : 0, cin, cout);
-  if (dtype == CNNITMO_F32 && !dgrad && tconv_ws_handles(0, cin, cout, true))
-    return tconv_ws_name(0, cin, cout, true);
+  if (dtype == CNNITMO_F32 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout, true))
+    return tconv_ws_name(dgrad ? 1 : 0, cin, cout, true);
   if (dtype == CNNITMO_BF16 && dgrad && tconv_kc_handles(cin, cout)) return tconv_kc_name(cin, cout);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
@@ -632,6 +632,9 @@ extern "C" int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h,
                            nullptr, (hipStream_t)stream, "tconv2x2_dgrad");
   if (dtype == CNNITMO_BF16 && tconv_kc_handles(cin, cout))
     return launch_tconv_kc(dout, n, h, w, cout, kT, cin, dx, (hipStream_t)stream, "tconv2x2_dgrad");
+  if (dtype == CNNITMO_F32 && tconv_ws_handles(1, cin, cout, true))
+    return launch_tconv_ws(1, dout, cout, 0, kT, n, h, w, cin, cout, dx, cin, 0, nullptr, 0, nullptr, nullptr,
+                           nullptr, (hipStream_t)stream, "tconv2x2_dgrad", true);
   return dispatch(dtype, a, stream, "tconv2x2_dgrad");
 }
 

@@ -20,7 +20,8 @@
 //   inference affine, BN partial sums (per tile, DPP row sums added into the
 //   wave's LDS slice; one row per wave at the end: rows = tconv_ws_rows).
 // MODE 1 (input gradient): A row of input pixel (y, x) = the four dout pixels
-//   (2y+a, 2x+b) x cout (k = tap*cout + co), B = kT [cin][4*cout]; dx [P][cin].
+//   (2y+a, 2x+b) x cout (k = tap*cout + co), B = kT [cin][4*cout]; dx [P][cin] (bf16, or
+//   fp32 for fp32 training's up8 / up9).
 #include <cstdio>
 
 #include "igemm_common.h"
@@ -77,7 +78,6 @@ template <int MODE, int BN, int NKS, int FM = 2, int SQ = BN / 32, typename TE =
 __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   constexpr int FN = BN / 16, TP = 16 * FM;
   constexpr int ES = sizeof(TE), KE = 16 / ES, KS = 64 / ES;
-  static_assert(ES == 2 || MODE == 0, "fp32: the forward only (inference, or training with BN sums)");
   const TE* __restrict__ PA = (const TE*)p.a;
   const TE* __restrict__ PB = (const TE*)p.b;
   TE* __restrict__ PO = (TE*)p.out;
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
         ab[f] = PA + pc * p.a_ld + p.a_off + kq * KE;
       } else {
         const int pi = (int)pc, img = pi / hw, rem = pi - img * hw, y = rem / p.w, x = rem - y * p.w;
-        ab[f] = PA + (((size_t)img * 2 * p.h + 2 * y) * 2 * p.w + 2 * x) * p.cout + kq * 8;
+        ab[f] = PA + (((size_t)img * 2 * p.h + 2 * y) * 2 * p.w + 2 * x) * p.cout + kq * KE;
       }
     }
   };
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
       if constexpr (MODE == 0) {
         dst[f] = *reinterpret_cast<const uint4*>(ab[f] + ks * KS);
       } else {
-        const int k0 = ks * 32, tap = k0 / p.cout, co = k0 - tap * p.cout;
+        const int k0 = ks * KS, tap = k0 / p.cout, co = k0 - tap * p.cout;
         dst[f] = *reinterpret_cast<const uint4*>(ab[f] + ((tap >> 1) * 2 * p.w + (tap & 1)) * p.cout + co);
       }
     }
@@ -250,6 +250,15 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
               }
             }
           }
+        } else if constexpr (ES == 4) {  // fp32 input gradient: two 16-byte stores per (pixel, 8 channels)
+#pragma unroll
+          for (int f = 0; f < FM; ++f) {
+            if (px[f] < P) {
+              float4* d = reinterpret_cast<float4*>(PO + (size_t)px[f] * p.out_ld + p.out_off + nb * BN + qq * 32 + kq * 8);
+              d[0] = float4{acc[f][2 * qq][0], acc[f][2 * qq][1], acc[f][2 * qq][2], acc[f][2 * qq][3]};
+              d[1] = float4{acc[f][2 * qq + 1][0], acc[f][2 * qq + 1][1], acc[f][2 * qq + 1][2], acc[f][2 * qq + 1][3]};
+            }
+          }
         } else {
 #pragma unroll
           for (int f = 0; f < FM; ++f) {
@@ -335,10 +344,11 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
   }();
   if (!en || cout % 32 || cin % 32) return false;
   const int K = mode == 0 ? cin : 4 * cout, N = mode == 0 ? 4 * cout : cin;
-  if (f32) {  // fp32 inference forward: the widest block whose fp32 rows fit (K 512: 64, 256 / 128: 128)
+  if (f32) {  // fp32 forward: the widest block whose fp32 rows fit (K 512: 64, 256 / 128: 128)
     // K = 128 is up9 (128 -> 64 channels at full resolution), which ran on igemm_fwd2's
-    // 128 x 128 tiles at 0.49 of fp32 peak (a 256-column block spills: 16 fp32 fragments)
-    if (!en32 || mode != 0 || (K != 128 && K != 256 && K != 512)) return false;
+    // 128 x 128 tiles at 0.49 of fp32 peak (a 256-column block spills: 16 fp32 fragments).
+    // fp32 input gradient (training): K = 4 * cout = 256 (up9) / 512 (up8)
+    if (!en32 || (K != 128 && K != 256 && K != 512) || (mode == 1 && K == 128)) return false;
     const int bn = K == 512 ? 64 : 128;
     if (N % bn || N / bn > 32 || 32 % (N / bn)) return false;
     pl.bn = bn;
@@ -433,11 +443,16 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 64, 32, 2, 2, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 64, 32, 2, 2, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 16, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     return true;
   }();
   (void)attr;
 #define TWL(M, KS) hipLaunchKernelGGL((tconv_ws_kernel<M, 128, KS>), dim3(grid), dim3(NW * 64), lds, s, t)
-  if (f32) {  // K / 16 steps
+  if (f32 && mode == 1) {  // K / 16 steps
+    if (t.K == 512) hipLaunchKernelGGL((tconv_ws_kernel<1, 64, 32, 2, 2, float>), dim3(grid), dim3(NW * 64), lds, s, t);
+    else hipLaunchKernelGGL((tconv_ws_kernel<1, 128, 16, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
+  } else if (f32) {  // K / 16 steps
     if (t.K == 512) hipLaunchKernelGGL((tconv_ws_kernel<0, 64, 32, 2, 2, float>), dim3(grid), dim3(NW * 64), lds, s, t);
     else if (t.K == 256) hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 16, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
     else hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 8, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
