@@ -188,6 +188,11 @@ size_t wgrad_tconv_ws_bytes(int n, int h, int w, int cin, int cout);
 const char* wgrad_tconv_name(int n, int h, int w, int cin, int cout);
 int launch_wgrad_tconv(const bf16* x, long x_ld, int x_off, const bf16* dy, int n, int h, int w, int cin,
                        int cout, float* ws, size_t ws_bytes, hipStream_t s);
+// its fp32 form (64 x 64 channel blocks, scalar-read fragments)
+size_t wgrad_tconv_f32_ws_bytes(int n, int h, int w, int cin, int cout);
+const char* wgrad_tconv_f32_name(int n, int h, int w, int cin, int cout);
+int launch_wgrad_tconv_f32(const float* x, long x_ld, int x_off, const float* dy, int n, int h, int w, int cin,
+                           int cout, float* ws, size_t ws_bytes, hipStream_t s);
 // sliding-window bf16 3x3 weight gradient for the high-resolution layers, wgrad_halo.hip
 // (x2 != null: a concatenate's two members, channels [0, 32) from x and [32, cin) from x2)
 size_t wgrad_halo_ws_bytes(int n, int h, int w, int cin, int cout, bool cat = false);

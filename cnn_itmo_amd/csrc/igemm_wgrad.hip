@@ -495,7 +495,7 @@ extern "C" size_t cnnitmo_tconv2x2_wgrad_workspace_bytes(int dtype, int n, int h
                                                          int cout) {
   const long P = (long)n * h * w;
   return dtype == CNNITMO_BF16 ? std::max(ws_bytes_for<bf16>(P, cout, cin, 4), wgrad_tconv_ws_bytes(n, h, w, cin, cout))
-                               : ws_bytes_for<float>(P, cout, cin, 4);
+                               : std::max(ws_bytes_for<float>(P, cout, cin, 4), wgrad_tconv_f32_ws_bytes(n, h, w, cin, cout));
 }
 
 extern "C" int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
@@ -621,6 +621,16 @@ extern "C" int cnnitmo_tconv2x2_wgrad(int dtype, const void* x, const void* dout
       return cnnitmo_check_launch("tconv2x2_wgrad");
     }
   }
+  if (dtype == CNNITMO_F32) {
+    const int splits = launch_wgrad_tconv_f32((const float*)x, cin, 0, (const float*)dout, n, h, w, cin, cout,
+                                              (float*)workspace, ws_bytes, s);
+    if (splits > 0) {
+      int rc = cnnitmo_check_launch("tconv2x2_wgrad");
+      if (rc) return rc;
+      slab_reduce((const float*)workspace, 4L * cout * cin, splits, 4 * cout, cin, cin, dk, f, s);
+      return cnnitmo_check_launch("tconv2x2_wgrad");
+    }
+  }
   if (dtype == CNNITMO_BF16)
     return run_wgrad<bf16>(a, dk, 4 * cout, cin, cin, workspace, ws_bytes, s, "tconv2x2_wgrad", f, 1);
   if (dtype == CNNITMO_F32)
@@ -644,6 +654,10 @@ extern "C" const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, in
   }
   if (dtype == CNNITMO_BF16 && ntaps == 4) {
     const char* tn = wgrad_tconv_name(n, h, w, cin, cout);
+    if (tn[0]) return tn;
+  }
+  if (dtype == CNNITMO_F32 && ntaps == 4) {
+    const char* tn = wgrad_tconv_f32_name(n, h, w, cin, cout);
     if (tn[0]) return tn;
   }
   if (dtype == CNNITMO_F32 && ntaps == 9) {
