@@ -12,11 +12,14 @@
 #   bash tools/recipe.sh env      <tag> "<VAR=value>" <layers> <ops>  per-layer A/B under an environment switch
 #   bash tools/recipe.sh benchab  <tag> "<VAR=value>|<lib.so>" [bench args...]   bench A/B, interleaved twice
 #   bash tools/recipe.sh pmc      <tag> <layers> <ops> "<counters>"  one rocprofv3 --pmc pass over bench_layers
+#   bash tools/recipe.sh isolate  <tag> <test file> "<-k expr>" "<VAR=value>"...   one test under each switch
+#                                                              (baseline first); a test failure does not end the
+#                                                              call, a timeout / crash does
 #   bash tools/recipe.sh mfma     <tag> [bench args...]        MFMA-busy + GRBM_GUI_ACTIVE pass over one bench step
 #                                                              (post-process: python tools/mfma_busy.py <csv>)
 #
 # Variant libraries come from tools/build_variant.sh (CPU side, before the call).
-set -e
+set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 O=$R/gpurun_out
 LIB=$R/cnn_itmo_amd/lib/libcnnitmo.so
@@ -76,6 +79,16 @@ pmc)
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d "$O/pmc_$tag" -o run -- \
     python3 "$R/tools/bench_layers.py" --layers "$L" --ops "$P" --iters 1 > "$O/pmc_${tag}.log" 2>&1 ;;
+isolate)
+  f=$1; k=$2; shift 2
+  for e in "" "$@"; do
+    env $e timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread "$f" -k "$k" \
+      > "$O/${tag}_iso.log.tmp" 2>&1 && rc=0 || rc=$?
+    echo "== ${e:-baseline} rc=$rc: $(tail -1 "$O/${tag}_iso.log.tmp")"
+    cat "$O/${tag}_iso.log.tmp" >> "$O/${tag}_iso.log"
+    [ $rc -le 1 ] || exit $rc
+  done | tee "$O/${tag}_iso.txt"
+  rm -f "$O/${tag}_iso.log.tmp" ;;
 mfma)
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
