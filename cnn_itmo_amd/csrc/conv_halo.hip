@@ -938,10 +938,12 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   // dec9a's forward (cin 96 = the [conv1 32 | up9 64] concat, 64 output channels, one column
   // block): 8-row tiles with all three weight chunks resident (2 x 22 KB patches + 108 KB
   // weights) instead of 16-row tiles streaming 36 KB of weights per 32-channel item.
-  // CNNITMO_HALO_TH8=0: 16-row tiles
+  // Off by default (CNNITMO_HALO_TH8=1 enables it): 8.00 vs 7.85 ms on dec9a's forward
+  // (profiles/r04b_th8_ab.txt; twice the halo rows per output row, and half the MFMAs
+  // per barrier)
   static const int th8 = [] {
     const char* e = getenv("CNNITMO_HALO_TH8");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   pl.th = 16;
   if (th8 && !f32 && pl.epi == 1 && pl.bn == 64 && a.N == 64 && a.cin == 96 && !a.pool_out && res) {

@@ -183,10 +183,12 @@ __global__ __launch_bounds__(KC_NW * 64) void tconv_kc_kernel(const KCArgs p) {
   }
 }
 
+// Off by default (CNNITMO_TCONV_KC=1 enables it): parity-green, but 1.38 / 2.87 ms on
+// up6 / up7 against igemm_fwd2's 0.69 / 1.65 (profiles/r04b_kc_ab.txt)
 bool kc_plan(int cin, int cout, int& nblk, int& gpx) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_TCONV_KC");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   if (!en || (cout != 256 && cout != 512) || cin % KC_BN) return false;
   nblk = cin / KC_BN;
