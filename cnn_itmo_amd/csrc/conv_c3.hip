@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 
           for (int k = 0; k < 8; ++k) {
             float t = acc[k >> 2][k & 3] + bj[k];
             if (relu) t = fmaxf(t, 0.f);
-            if constexpr (AFF) t = t * sj[k] + hj[k];
+            if constexpr (AFF) t = fmaf(t, sj[k], hj[k]);  // (explicit: the same rounding for every fragment)
             v[k] = t;
             const float vs = ok ? t : 0.f;
             s1[k] += vs;

@@ -71,7 +71,10 @@ constexpr int PFT = 5;
 // tap offset of the DMA issue window for waves NWAVE/2.. (the second wave on each SIMD):
 // the two waves of a SIMD then issue their pieces in different taps
 // EPI 2 (bf16): issue the epilogue's r loads during the tile's last tap (1) or after its
-// MFMAs (0)
+// MFMAs (0).  1 compiles without spills (sums in per-wave LDS slots, 240-255 VGPRs) and is
+// parity-green, but measured 15-20 % slower on every fused dgrad (dec6-dec9b 38.2 -> 44.9 ms,
+// profiles/r04e_rtap_ab.txt): the last tap's MFMAs do not cover an HBM load, and the slot
+// read-modify-writes and row reductions add LDS and VALU work to every tile.
 #ifndef HALO_RTAP
 #define HALO_RTAP 0
 #endif
@@ -446,7 +449,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           }
           if (aff) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = v[k] * sj[k] + hj[k];
+            for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sj[k], hj[k]);
           }
 #pragma unroll
           for (int k = 0; k < 8; ++k) {

@@ -280,7 +280,7 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
           for (int k = 0; k < 8; ++k) {
             float v = acc[f][2 * jp + (k >> 2)][k & 3] + bj[k];
             if (relu) v = fmaxf(v, 0.f);
-            if (aff) v = v * sj[k] + hj[k];
+            if (aff) v = fmaf(v, sj[k], hj[k]);
             const float vs = ok ? v : 0.f;
             s1[jp][k] += vs;
             s2[jp][k] += vs * vs;

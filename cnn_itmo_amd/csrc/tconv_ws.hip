@@ -231,7 +231,7 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
             for (int k = 0; k < 8; ++k) {
               float v = acc[f][2 * qq + (k >> 2)][k & 3] + bj[k];
               if (relu) v = fmaxf(v, 0.f);
-              if (aff) v = v * sj[k] + hj[k];
+              if (aff) v = fmaf(v, sj[k], hj[k]);
               const float vs = ok ? v : 0.f;
               s1[qq % SQ][k] += vs;
               s2[qq % SQ][k] += vs * vs;
