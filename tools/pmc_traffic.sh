@@ -21,3 +21,4 @@ run train "train 1080x1920 b32 bfloat16"
 run infer8 "infer 1080x1920 b8 float32" --mode infer --dtype float32 --batch 8
 run infer32 "infer 1080x1920 b32 float32" --mode infer --dtype float32 --batch 32
 run train4k "train 2160x3840 b8 bfloat16" --height 2160 --width 3840 --batch 8
+run train32 "train 1080x1920 b8 float32" --dtype float32 --batch 8
