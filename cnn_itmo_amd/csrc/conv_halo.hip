@@ -412,9 +412,9 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const size_t pofs = (((size_t)e.img * (p.ho / 2) + oh0 / 2) * (p.wo / 2) + e.x0 / 2) * p.pool_ld + n0;
     const __amdgpu_buffer_rsrc_t ps = dma::brsrc(POOL ? (const TE*)p.pool_out + pofs : obase);
     const __amdgpu_buffer_rsrc_t pis = dma::brsrc(POOL ? (const unsigned char*)p.pool_idx + pofs : (const unsigned char*)obase);
-    // POOL: the window rows' values as stored (bf16: the packed store operand, 4 VGPRs a row)
-    float vr[ES == 4 ? 2 : 1][8];
-    dma::i32x4 vrp[2];
+    // POOL: the running maximum of the lane's window (value and window index per channel)
+    float pb[8];
+    unsigned pa[2] = {0u, 0u};
 #pragma unroll
     for (int q = 0; q < FP; ++q) {
       const int cl = 32 * q + 8 * g;  // the lane's first column in the block
@@ -458,6 +458,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
             sb[q][k] += vs * vs;
           }
         }
+        dma::i32x4 pk8{};
         if constexpr (LINES) {
           pk[q][f] = pack8(v);
         } else if constexpr (ES == 4) {
@@ -467,54 +468,51 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, hi), os, ok ? off + 16 : OOB, 0, 0);
         } else {
           const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 2);
-          const dma::i32x4 pk8 = pack8(v);
+          pk8 = pack8(v);
           __builtin_amdgcn_raw_buffer_store_b128(pk8, os, ok ? off : OOB, 0, 0);
-          if constexpr (POOL) vrp[rl] = pk8;
         }
         if constexpr (POOL) {
+          // this window row as stored: the lane's pixel (tl) and its right neighbour (tr, DPP
+          // quad_perm xor 1); a running maximum over the rows in window order (0,0), (0,1),
+          // (1,0), (1,1), the first maximum winning (strict compares)
+          float tl[8], tr[8];
           if constexpr (ES == 4) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) vr[rl][k] = v[k];
-          }
-          if (rl == 1) {  // window row complete: (0,0),(0,1) = row 0 here and right; (1,0),(1,1) = row 1
-            float pv[8], w0[8], w1[8], w2[8], w3[8];
-            if constexpr (ES == 4) {
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                w0[k] = vr[0][k];
-                w2[k] = vr[1][k];
-                w1[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w0[k]), 0xB1, 0xF, 0xF, false));
-                w3[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(w2[k]), 0xB1, 0xF, 0xF, false));
-              }
-            } else {  // the neighbour's packed rows by DPP (4 dwords each), then unpacked
-              dma::i32x4 n0v, n1v;
-#pragma unroll
-              for (int d = 0; d < 4; ++d) {
-                n0v[d] = __builtin_amdgcn_update_dpp(0, vrp[0][d], 0xB1, 0xF, 0xF, false);
-                n1v[d] = __builtin_amdgcn_update_dpp(0, vrp[1][d], 0xB1, 0xF, 0xF, false);
-              }
-              const bf16x8 b0 = __builtin_bit_cast(bf16x8, vrp[0]), b1 = __builtin_bit_cast(bf16x8, n0v);
-              const bf16x8 b2 = __builtin_bit_cast(bf16x8, vrp[1]), b3 = __builtin_bit_cast(bf16x8, n1v);
-#pragma unroll
-              for (int k = 0; k < 8; ++k) {
-                w0[k] = to_f32(b0[k]);
-                w1[k] = to_f32(b1[k]);
-                w2[k] = to_f32(b2[k]);
-                w3[k] = to_f32(b3[k]);
-              }
+            for (int k = 0; k < 8; ++k) {
+              tl[k] = v[k];
+              tr[k] = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[k]), 0xB1, 0xF, 0xF, false));
             }
-            unsigned pa[2] = {0u, 0u};
+          } else {  // bf16: the packed store operand and the neighbour's (4 dwords by DPP), unpacked
+            dma::i32x4 nb;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) nb[d] = __builtin_amdgcn_update_dpp(0, pk8[d], 0xB1, 0xF, 0xF, false);
+            const bf16x8 bl = __builtin_bit_cast(bf16x8, pk8), br = __builtin_bit_cast(bf16x8, nb);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-              const float t0 = w0[k], t1 = w1[k], t2 = w2[k], t3 = w3[k];
-              float best = t0, kb = md[k] * t0;
-              unsigned a = 0;
-              if (md[k] * t1 > kb) { kb = md[k] * t1; best = t1; a = 1; }
-              if (md[k] * t2 > kb) { kb = md[k] * t2; best = t2; a = 2; }
-              if (md[k] * t3 > kb) { best = t3; a = 3; }
-              pv[k] = best;
-              pa[k >> 2] |= a << (8 * (k & 3));
+              tl[k] = to_f32(bl[k]);
+              tr[k] = to_f32(br[k]);
             }
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const unsigned sh = 8 * (k & 3);
+            float best;
+            unsigned a;
+            if (rl == 0) {
+              best = tl[k];
+              a = 0;
+              if (md[k] * tr[k] > md[k] * best) { best = tr[k]; a = 1; }
+            } else {
+              best = pb[k];
+              a = (pa[k >> 2] >> sh) & 0xFFu;
+              if (md[k] * tl[k] > md[k] * best) { best = tl[k]; a = 2; }
+              if (md[k] * tr[k] > md[k] * best) { best = tr[k]; a = 3; }
+            }
+            pb[k] = best;
+            pa[k >> 2] = (pa[k >> 2] & ~(0xFFu << sh)) | (a << sh);
+          }
+          if (rl == 1) {  // window complete
+            const float* pv = pb;
             const bool pok = (pxl & 1) == 0 && oh0 + 2 * rp < p.ho && e.x0 + cb * 16 + pxl < p.wo;
             const unsigned pe = (unsigned)((rp * (p.wo / 2) + cb * 8 + (pxl >> 1)) * p.pool_ld + cl);  // elements
             if constexpr (ES == 4) {
