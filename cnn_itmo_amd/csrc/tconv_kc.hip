@@ -31,7 +31,16 @@
 
 namespace {
 
-constexpr int KC_NW = 8, KC_BN = 128, KC_KSC = 8, KC_FM = 2, KC_PD = 4;
+#ifndef KC_DEFAULT_ON
+#define KC_DEFAULT_ON 0
+#endif
+#ifndef KC_FM_DEF
+#define KC_FM_DEF 2
+#endif
+#ifndef KC_PD_DEF
+#define KC_PD_DEF 4
+#endif
+constexpr int KC_NW = 8, KC_BN = 128, KC_KSC = 8, KC_FM = KC_FM_DEF, KC_PD = KC_PD_DEF;
 constexpr int KC_TP = 16 * KC_FM * KC_NW;       // pixels per pass
 constexpr int KC_CHUNK = KC_KSC * KC_BN * 64;   // bytes per weight chunk (64 KB)
 constexpr int KC_BPT = KC_CHUNK / 16 / (KC_NW * 64);  // 16-byte weight pieces per thread per chunk (8)
@@ -188,7 +197,7 @@ __global__ __launch_bounds__(KC_NW * 64) void tconv_kc_kernel(const KCArgs p) {
 bool kc_plan(int cin, int cout, int& nblk, int& gpx) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_TCONV_KC");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : KC_DEFAULT_ON;
   }();
   if (!en || (cout != 256 && cout != 512) || cin % KC_BN) return false;
   nblk = cin / KC_BN;
