@@ -688,6 +688,7 @@ def infer_leg(args, rank, world, timer, barrier, agree, P_init, H, W, B, with_cp
            "roofline": roof, "cpu_baseline": None}
     if rank == 0:
         _print_agg(agg, f"infer b{B}")
+        _print_detail(timer.detail(), k2, f"infer b{B}")
         if world == 1 and not args.no_cpu and with_cpu:
             try:
                 out["cpu_baseline"] = cpu_baseline(args, P, H, W, train=False)
