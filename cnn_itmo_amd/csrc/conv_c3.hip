@@ -74,6 +74,9 @@ struct C3Fwd2 {
   float* stats;  // [gridDim.x][2][32]
 };
 
+#ifndef C3_F32_LINES
+#define C3_F32_LINES 1                      // fp32 stores as whole 128-byte lines (line_pair)
+#endif
 #ifndef C3_MINW
 #define C3_MINW 3                           // waves per SIMD the register budget is sized for
 #endif
@@ -220,7 +223,18 @@ __global__ __launch_bounds__(256, C3_MINW) void conv_c3_fwd_kernel(const C3Fwd2 
             s1[k] += vs;
             s2[k] += vs * vs;
           }
-          if (ok) {
+          if constexpr (F32 && C3_F32_LINES) {
+            // a pixel's 32 fp32 channels are one 128-byte line: after one DPP exchange
+            // (line_pair) store 1 writes pixels 0-7 and store 2 pixels 8-15 of the fragment
+            // as whole lines (lane (pxl, g): channels 8g + 4*(pxl >> 3) .. +3)
+            const uint4 lo = __builtin_bit_cast(uint4, float4{v[0], v[1], v[2], v[3]});
+            const uint4 hi = __builtin_bit_cast(uint4, float4{v[4], v[5], v[6], v[7]});
+            uint4 v1, v2;
+            line_pair(lo, hi, pxl, v1, v2);
+            const int q1 = p0 + f * 16 + (pxl & 7), q2 = q1 + 8, c = 8 * g + 4 * (pxl >> 3);
+            if (q1 < npx) *reinterpret_cast<uint4*>((float*)a.out + (prow + q1) * a.out_ld + a.out_off + c) = v1;
+            if (q2 < npx) *reinterpret_cast<uint4*>((float*)a.out + (prow + q2) * a.out_ld + a.out_off + c) = v2;
+          } else if (ok) {
             TO* o = (TO*)a.out + (prow + px) * a.out_ld + a.out_off + 8 * g;
             Pack16<TO>::store(o, v);
             if constexpr (F32) Pack16<TO>::store(o + 4, v + 4);

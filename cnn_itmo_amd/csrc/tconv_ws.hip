@@ -38,6 +38,9 @@ constexpr int WS_PAD = 32;
 #ifndef TWS_LINES
 #define TWS_LINES 1
 #endif
+#ifndef TWS_F32_LINES
+#define TWS_F32_LINES 1
+#endif
 #ifndef TWS_PD
 #define TWS_PD 4  // A K-steps in flight per wave (3: 9.64, 4: 9.48, 6: 9.56 ms over up6-up8 fwd+dgrad)
 #endif
@@ -153,6 +156,38 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
   // in registers for the whole launch (one DPP reduction at the end instead of one per
   // tile: the per-tile reduction was as much VALU issue as the tile's MFMAs)
   constexpr int FP = FN / 2;
+  // fp32 output of (fragment base pixel pb, block column pair qq): a pair is 32 channels = one
+  // 128-byte line per pixel.  TWS_F32_LINES: one DPP exchange (line_pair) so that store 1
+  // writes pixels pb..pb+7 and store 2 pixels pb+8..pb+15 as whole lines (lane (frow, kq):
+  // 16 bytes at channel kq*8 + 4*(frow >> 3) of pixel pb + (frow & 7) / + 8); otherwise
+  // each lane's two 16-byte pieces of its own pixel (half lines per instruction)
+  auto dst32 = [&](long pi, int c) -> float* {  // block column c of pixel pi
+    const int n = nb * BN + c;
+    if constexpr (MODE == 0) {
+      const int tap = n / p.cout, co = n - tap * p.cout;
+      const int ip = (int)pi, img = ip / hw, rem = ip - img * hw, y = rem / p.w, x = rem - y * p.w;
+      const size_t op = ((size_t)img * 2 * p.h + 2 * y + (tap >> 1)) * 2 * p.w + 2 * x + (tap & 1);
+      return (float*)PO + op * p.out_ld + p.out_off + co;
+    } else {
+      return (float*)PO + (size_t)pi * p.out_ld + p.out_off + n;
+    }
+  };
+  auto st32 = [&](long pb, long pix, bool ok, int qq, const float* vf) {
+    const uint4 a = __builtin_bit_cast(uint4, float4{vf[0], vf[1], vf[2], vf[3]});
+    const uint4 b = __builtin_bit_cast(uint4, float4{vf[4], vf[5], vf[6], vf[7]});
+    if constexpr (TWS_F32_LINES) {
+      uint4 v1, v2;
+      line_pair(a, b, frow, v1, v2);
+      const int c = qq * 32 + kq * 8 + 4 * (frow >> 3);
+      const long p1 = pb + (frow & 7), p2 = p1 + 8;
+      if (p1 < P) *reinterpret_cast<uint4*>(dst32(p1, c)) = v1;
+      if (p2 < P) *reinterpret_cast<uint4*>(dst32(p2, c)) = v2;
+    } else if (ok) {
+      uint4* d = reinterpret_cast<uint4*>(dst32(pix, qq * 32 + kq * 8));
+      d[0] = a;
+      d[1] = b;
+    }
+  };
   float s1[MODE == 0 ? SQ : 1][8], s2[MODE == 0 ? SQ : 1][8];
 #pragma unroll
   for (int q = 0; q < (MODE == 0 ? SQ : 1); ++q)
@@ -239,25 +274,15 @@ __global__ __launch_bounds__(NW * 64) void tconv_ws_kernel(const WSArgs p) {
               vf[k] = v;
             }
             pk[hq][f] = __builtin_bit_cast(uint4, o);
-            if constexpr (ES == 4) {  // fp32: 8 channels = two 16-byte stores, no line exchange
-              if (ok) {
-                const int n = nb * BN + qq * 32 + kq * 8, tap = n / p.cout, co = n - tap * p.cout;
-                const int ip = (int)px[f], img = ip / hw, rem = ip - img * hw, y = rem / p.w, x = rem - y * p.w;
-                const size_t op = ((size_t)img * 2 * p.h + 2 * y + (tap >> 1)) * 2 * p.w + 2 * x + (tap & 1);
-                float4* d = reinterpret_cast<float4*>(PO + op * p.out_ld + p.out_off + co);
-                d[0] = float4{vf[0], vf[1], vf[2], vf[3]};
-                d[1] = float4{vf[4], vf[5], vf[6], vf[7]};
-              }
-            }
+            if constexpr (ES == 4) st32(t * TP + f * 16, px[f], ok, qq, vf);
           }
-        } else if constexpr (ES == 4) {  // fp32 input gradient: two 16-byte stores per (pixel, 8 channels)
+        } else if constexpr (ES == 4) {  // fp32 input gradient
 #pragma unroll
           for (int f = 0; f < FM; ++f) {
-            if (px[f] < P) {
-              float4* d = reinterpret_cast<float4*>(PO + (size_t)px[f] * p.out_ld + p.out_off + nb * BN + qq * 32 + kq * 8);
-              d[0] = float4{acc[f][2 * qq][0], acc[f][2 * qq][1], acc[f][2 * qq][2], acc[f][2 * qq][3]};
-              d[1] = float4{acc[f][2 * qq + 1][0], acc[f][2 * qq + 1][1], acc[f][2 * qq + 1][2], acc[f][2 * qq + 1][3]};
-            }
+            float vf[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) vf[k] = acc[f][2 * qq + (k >> 2)][k & 3];
+            st32(t * TP + f * 16, px[f], px[f] < P, qq, vf);
           }
         } else {
 #pragma unroll
