@@ -75,8 +75,9 @@ struct C3Fwd2 {
 };
 
 #ifndef C3_F32_LINES
-#define C3_F32_LINES 1                      // fp32 stores as whole 128-byte lines (line_pair)
-#endif
+#define C3_F32_LINES 0                      // fp32 stores as whole 128-byte lines (line_pair): neutral
+#endif                                      // in the fp32 inference step and 23 VGPRs of spill
+                                            // (profiles/r04o_c3_ab.txt), off by default
 #ifndef C3_MINW
 #define C3_MINW 3                           // waves per SIMD the register budget is sized for
 #endif

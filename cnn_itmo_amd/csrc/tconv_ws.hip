@@ -38,8 +38,10 @@ constexpr int WS_PAD = 32;
 #ifndef TWS_LINES
 #define TWS_LINES 1
 #endif
+// fp32 stores as whole lines: measured slower in the fp32 inference step (98.0-98.2 vs
+// 98.6-98.7 frames/s, profiles/r04o_ws_ab.txt), off by default
 #ifndef TWS_F32_LINES
-#define TWS_F32_LINES 1
+#define TWS_F32_LINES 0
 #endif
 #ifndef TWS_PD
 #define TWS_PD 4  // A K-steps in flight per wave (3: 9.64, 4: 9.48, 6: 9.56 ms over up6-up8 fwd+dgrad)
