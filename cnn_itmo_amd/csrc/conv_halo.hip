@@ -140,7 +140,9 @@ struct HaloArgs {
 // and s * (min r) + h where gamma < 0: the kernel pools r by the per-channel mode sign(gamma)
 // (pool_sign), and the pooled value is itself a folded value.  Inference stores y (AFFINE)
 // and pools it by its maximum.
-template <typename TE, int BN, int EPI, bool RES, bool POOL = false, int THT = 16>
+// NOSUM (EPI 1): no BN partial sums (the inference forward): the 2 x FP x 8 accumulators live across
+// the whole launch otherwise
+template <typename TE, int BN, int EPI, bool RES, bool POOL = false, int THT = 16, bool NOSUM = false>
 __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   using C = HCfg<BN, RES, THT>;
   constexpr int TH = THT, RPW = TH / NWAVE, FM = RPW * FMR, PROWS = (TH + 2) * PW;  // (shadow the 16-row defaults)
@@ -376,7 +378,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   };
   // BN partial sums of the lane's pixels for its 8 channels of each pair (EPI 1), or
   // sums of dz by pixel-row parity (EPI 2; the lane's pixel-column parity is lane & 1)
-  constexpr int NSUM = EPI == 0 || SLOT ? 1 : FP;
+  constexpr int NSUM = EPI == 0 || SLOT || NOSUM ? 1 : FP;
   float sa[NSUM][8], sb[NSUM][8];
 #pragma unroll
   for (int q = 0; q < NSUM; ++q)
@@ -451,11 +453,13 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sj[k], hj[k]);
           }
+          if constexpr (!NOSUM) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float vs = ok ? v[k] : 0.f;
-            sa[q][k] += vs;
-            sb[q][k] += vs * vs;
+            for (int k = 0; k < 8; ++k) {
+              const float vs = ok ? v[k] : 0.f;
+              sa[q][k] += vs;
+              sb[q][k] += vs * vs;
+            }
           }
         }
         dma::i32x4 pk8{};
@@ -786,7 +790,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 
   // partial-sum rows: one per (stream, wave); the 16 pixel lanes are folded here
   const long row = (long)gs * NWAVE + wave;
-  if constexpr (EPI == 1) {
+  if constexpr (EPI == 1 && !NOSUM) {
     if (p.flags & CNNITMO_STATS) {
 #pragma unroll
       for (int q = 0; q < FP; ++q)
@@ -963,9 +967,20 @@ void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s, int th = 1
     }
   }
   if constexpr (EPI == 1) {
+    const bool nst = !(h.f.flags & CNNITMO_STATS);  // inference: the kernels without BN sums
     if (h.f.pool_out) {
-      if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
-      else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true>), dim3(grid), dim3(NT), 0, s, h);
+      if (nst) {
+        if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true, 16, true>), dim3(grid), dim3(NT), 0, s, h);
+        else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true, 16, true>), dim3(grid), dim3(NT), 0, s, h);
+      } else {
+        if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
+        else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true>), dim3(grid), dim3(NT), 0, s, h);
+      }
+      return;
+    }
+    if (nst) {
+      if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, false, 16, true>), dim3(grid), dim3(NT), 0, s, h);
+      else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, false, 16, true>), dim3(grid), dim3(NT), 0, s, h);
       return;
     }
   }

@@ -48,7 +48,7 @@ def unmangle(n):
 
 def label(name):
     n = unmangle(name.replace(" ", "")).replace("(anonymousnamespace)::", "")
-    m = re.search(r"halo_conv_kernel<(?:(__bf16|float),)?(\d+),(\d+)(?:,(true|false))?(?:,(true|false))?(?:,(\d+))?>", n)
+    m = re.search(r"halo_conv_kernel<(?:(__bf16|float),)?(\d+),(\d+)(?:,(true|false))?(?:,(true|false))?(?:,(\d+))?(?:,(?:true|false))?>", n)
     if m:
         return "halo_conv_kernel<%s%s,%s%s%s%s>" % ("f32," if m.group(1) == "float" else "", m.group(2), m.group(3),
                                                    ",wres" if m.group(4) == "true" else "",
