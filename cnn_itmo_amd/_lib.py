@@ -47,6 +47,9 @@ SIGNATURES = {
     "cnnitmo_conv3x3_fwd_pool": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp, i32, i32, i32, vp, vp, vp,
                                        vp, vp, i32, vp, vp, vp]),
     "cnnitmo_conv3x3_pool_supported": (i32, [i32] * 6),
+    "cnnitmo_conv3x3_fwd_head": (i32, [i32, vp, i32, i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, vp, i32, vp, vp,
+                                       vp, vp]),
+    "cnnitmo_conv3x3_head_supported": (i32, [i32] * 6),
     "cnnitmo_pool_bnsums_pooled": (i32, [i32, vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]),
     "cnnitmo_wgrad_cat_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32]),
     "cnnitmo_wgrad_cat_kernel_name": (C.c_char_p, [i32, i32, i32, i32, i32, i32]),

@@ -152,7 +152,9 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   constexpr int ES = sizeof(TE), CC = 64 / ES, PE = 16 / ES;
   static_assert(!POOL || (EPI == 1 && RPW % 2 == 0), "pooling: the forward epilogue, whole window rows per wave");
   // stores per wave per epilogue (+ POOL: a value and an index store per window row and column block)
-  constexpr int NST = C::NST * (ES == 4 ? 2 : 1) + (POOL ? FP * (RPW / 2) * FMR * (ES == 4 ? 3 : 2) : 0);
+  // (EPI 3: three 4-byte yhat stores per fragment instead of the output rows)
+  constexpr int NST = EPI == 3 ? FM * 3
+                               : C::NST * (ES == 4 ? 2 : 1) + (POOL ? FP * (RPW / 2) * FMR * (ES == 4 ? 3 : 2) : 0);
   // EPI 2 with HALO_RTAP: the dz parity sums live in per-wave LDS slots [NWAVE][4][BN] (over
   // the border table, which EPI 2 does not use) instead of 32 registers
   constexpr bool SLOT = HALO_RTAP && EPI == 2 && ES == 2;
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   float* par = reinterpret_cast<float*>(smem + C::PAR);
   float* utb = reinterpret_cast<float*>(smem + C::UTB);
   // the workgroup's epilogue parameters (ordered before any epilogue by the ring barrier)
-  if constexpr (EPI == 1) {
+  if constexpr (EPI == 1 || EPI == 3) {
     const bool aff = p.flags & CNNITMO_AFFINE;
     for (int i = tid; i < 4 * BN; i += NT) {
       const int k = i / BN, c = n0 + i % BN;
@@ -190,7 +192,11 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       par[i] = k == 0 ? (p.bias ? p.bias[c] : 0.f) : k == 1 ? (aff ? p.aff_scale[c] : 1.f)
              : k == 2 ? (aff ? p.aff_shift[c] : 0.f) : (sg > 0.f ? 1.f : (sg < 0.f ? -1.f : 0.f));
     }
-    for (int i = tid; i < 8 * BN; i += NT) utb[i] = p.border ? p.border[(size_t)n0 * 8 + i] : 0.f;
+    if constexpr (EPI == 3) {  // the head: weights [3][BN] and bias [3] over the border table
+      for (int i = tid; i < 3 * BN + 3; i += NT) utb[i] = i < 3 * BN ? p.head_w[i] : p.head_b[i - 3 * BN];
+    } else {
+      for (int i = tid; i < 8 * BN; i += NT) utb[i] = p.border ? p.border[(size_t)n0 * 8 + i] : 0.f;
+    }
   } else if constexpr (EPI == 2) {
     const int cbn = p.bnb_c1 - p.bnb_c0;
     for (int i = tid; i < 3 * BN; i += NT) {
@@ -378,7 +384,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   };
   // BN partial sums of the lane's pixels for its 8 channels of each pair (EPI 1), or
   // sums of dz by pixel-row parity (EPI 2; the lane's pixel-column parity is lane & 1)
-  constexpr int NSUM = EPI == 0 || SLOT || NOSUM ? 1 : FP;
+  constexpr int NSUM = EPI == 0 || EPI == 3 || SLOT || NOSUM ? 1 : FP;
   float sa[NSUM][8], sb[NSUM][8];
 #pragma unroll
   for (int q = 0; q < NSUM; ++q)
@@ -417,14 +423,24 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     // POOL: the running maximum of the lane's window (value and window index per channel)
     float pb[8];
     unsigned pa[2] = {0u, 0u};
+    // EPI 3: the head's three dot products of each fragment's pixels, this lane's 16 channels
+    float zf[EPI == 3 ? FM : 1][3];
+    if constexpr (EPI == 3) {
+#pragma unroll
+      for (int f = 0; f < FM; ++f) zf[f][0] = zf[f][1] = zf[f][2] = 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < FP; ++q) {
       const int cl = 32 * q + 8 * g;  // the lane's first column in the block
-      float bj[8], sj[8], hj[8], md[8];
-      if constexpr (EPI == 1) {
+      float bj[8], sj[8], hj[8], md[8], hw[EPI == 3 ? 3 : 1][8];
+      if constexpr (EPI == 1 || EPI == 3) {
         lds8(par + cl, bj);
         lds8(par + BN + cl, sj);
         lds8(par + 2 * BN + cl, hj);
+      }
+      if constexpr (EPI == 3) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) lds8(utb + j * BN + cl, hw[j]);
       }
       if constexpr (POOL) lds8(par + 3 * BN + cl, md);
 #pragma unroll
@@ -438,7 +454,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
         float v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = acc[f][2 * q + (k >> 2)][k & 3];
-        if constexpr (EPI == 1) {
+        if constexpr (EPI == 1 || EPI == 3) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += bj[k];
           if (bt && (oh == 0 || oh == p.ho - 1 || ow == 0 || ow == p.wo - 1)) {
@@ -453,7 +469,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sj[k], hj[k]);
           }
-          if constexpr (!NOSUM) {
+          if constexpr (!NOSUM && EPI == 1) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
               const float vs = ok ? v[k] : 0.f;
@@ -463,7 +479,12 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           }
         }
         dma::i32x4 pk8{};
-        if constexpr (LINES) {
+        if constexpr (EPI == 3) {
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) zf[f][j] = fmaf(v[k], hw[j][k], zf[f][j]);
+        } else if constexpr (LINES) {
           pk[q][f] = pack8(v);
         } else if constexpr (ES == 4) {
           const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 4);
@@ -529,6 +550,26 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
             typedef int i32x2_ __attribute__((ext_vector_type(2)));
             __builtin_amdgcn_raw_buffer_store_b64(i32x2_{(int)pa[0], (int)pa[1]}, pis, pok ? pe : OOB, 0, 0);
           }
+        }
+      }
+    }
+    if constexpr (EPI == 3) {
+      // the 64 channels of a pixel sit on the 4 lane groups (lanes pxl + 16 g): two exchanges
+      // complete the dot products, then group 0 writes sigmoid(z + b) as 3 floats
+      const __amdgpu_buffer_rsrc_t ys = dma::brsrc(p.yhat);
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
+        const int oh = oh0 + rr, ow = e.x0 + col;
+        const bool ok = g == 0 && oh < p.head_hv && ow < p.wo;
+        const unsigned yo = (unsigned)((((long)e.img * p.head_hv + oh) * p.wo + ow) * 12);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          float z = zf[f][j];
+          z += __shfl_xor(z, 16, 64);
+          z += __shfl_xor(z, 32, 64);
+          const float yv = 1.f / (1.f + expf(-(z + utb[3 * BN + j])));
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_int(yv), ys, ok ? yo + 4 * j : OOB, 0, 0);
         }
       }
     }
@@ -931,6 +972,11 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
         a.bnb_r_ld % 8 || a.bnb_r_off % 8)
       return false;
     pl.epi = 2;
+  } else if (a.yhat) {  // the forward with the sigmoid head (one 64-column block: all channels)
+    if (a.N != 64 || pl.bn != 64 || a.a2 || a.pool_out || a.stats || a.border || (a.flags & CNNITMO_STATS) ||
+        !a.head_w || !a.head_b)
+      return false;
+    pl.epi = 3;
   } else {
     pl.epi = (a.flags || a.bias || a.border || a.stats) ? 1 : 0;
     if (a.a2 && pl.epi != 1) return false;  // two sources: the forward-epilogue kernels only
@@ -1012,7 +1058,9 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
   CNN_REQUIRE(h.tiles * h.nchunks < (1L << 31), "%s: too many tiles", what);
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
   const int grid = halo_ncu();
-  if (f32 && pl.epi == 1) {
+  if (f32 && pl.epi == 3) {
+    launch_cfg<float, 64, 3>(h, pl.res, grid, s);
+  } else if (f32 && pl.epi == 1) {
     if (pl.bn == 64) launch_cfg<float, 64, 1>(h, pl.res, grid, s);
     else launch_cfg<float, 32, 1>(h, pl.res, grid, s);
   } else if (f32 && pl.epi == 2) {
@@ -1024,6 +1072,8 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
   } else if (pl.epi == 2) {
     if (pl.bn == 64) launch_cfg<bf16, 64, 2>(h, pl.res, grid, s);
     else launch_cfg<bf16, 32, 2>(h, pl.res, grid, s);
+  } else if (pl.epi == 3) {
+    launch_cfg<bf16, 64, 3>(h, pl.res, grid, s);
   } else if (pl.epi == 1) {
     if (pl.bn == 64) launch_cfg<bf16, 64, 1>(h, pl.res, grid, s, pl.th);
     else launch_cfg<bf16, 32, 1>(h, pl.res, grid, s);

@@ -50,6 +50,13 @@ struct FwdArgs {
   long pool_ld;
   unsigned char* pool_idx;
   const float* pool_sign;
+  // the sigmoid head fused into the forward epilogue (halo kernel, EPI 3; inference): yhat
+  // [n][head_hv][wo][3] fp32 = sigmoid(y . head_w[3][N] + head_b), y (the conv's epilogue
+  // output) never stored
+  const float* head_w;
+  const float* head_b;
+  float* yhat;
+  int head_hv;
 };
 
 // Out-of-bounds-tap correction for a folded BN shift (see cnnitmo_fold_conv3x3):

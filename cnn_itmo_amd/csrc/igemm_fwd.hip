@@ -416,6 +416,44 @@ extern "C" int cnnitmo_conv3x3_pool_supported(int dtype, int n, int h, int w, in
   return halo_handles(a, f32) ? 1 : 0;
 }
 
+extern "C" int cnnitmo_conv3x3_fwd_head(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w,
+                                        int cin, const void* wt, const float* bias, int cout, int flags,
+                                        const float* aff_scale, const float* aff_shift, int h_valid,
+                                        const float* head_w, const float* head_b, float* yhat, void* stream) {
+  FwdArgs a = base_args();
+  a.a = x; a.a_ld = x_ld; a.a_off = x_off;
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cin; a.b = wt; a.N = cout; a.M = (long)n * h * w;
+  a.bias = bias; a.out_ld = cout; a.cout = cout;
+  a.flags = flags; a.aff_scale = aff_scale; a.aff_shift = aff_shift;
+  a.head_w = head_w; a.head_b = head_b; a.yhat = yhat; a.head_hv = h_valid;
+  CNN_REQUIRE(head_w && head_b && yhat, "conv3x3_fwd_head: missing head buffers");
+  CNN_REQUIRE(h_valid > 0 && h_valid <= h, "conv3x3_fwd_head: bad h_valid");
+  CNN_REQUIRE((long)n * h_valid * w * 12 < (1L << 31), "conv3x3_fwd_head: yhat too large for 32-bit offsets");
+  CNN_REQUIRE(!(flags & CNNITMO_STATS), "conv3x3_fwd_head: the inference forward has no BN sums");
+  CNN_REQUIRE(!(flags & CNNITMO_AFFINE) || (aff_scale && aff_shift), "conv3x3_fwd_head: AFFINE without coefficients");
+  const bool f32 = dtype == CNNITMO_F32;
+  if ((dtype != CNNITMO_BF16 && !f32) || !halo_handles(a, f32)) {
+    cnnitmo_set_error("conv3x3_fwd_head: unsupported (halo kernel, 64 output channels)");
+    return CNNITMO_EUNSUPPORTED;
+  }
+  return launch_halo(a, (hipStream_t)stream, "conv3x3_fwd_head", f32);
+}
+
+extern "C" int cnnitmo_conv3x3_head_supported(int dtype, int n, int h, int w, int cin, int cout) {
+  FwdArgs a = base_args();
+  a.a = (const void*)16; a.a_ld = cin;
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  set_taps3x3(a);
+  a.cin = cin; a.N = cout; a.M = (long)n * h * w; a.out_ld = cout; a.cout = cout;
+  a.flags = CNNITMO_RELU | CNNITMO_AFFINE;
+  a.head_w = a.head_b = (const float*)16; a.yhat = (float*)16; a.head_hv = h;
+  const bool f32 = dtype == CNNITMO_F32;
+  if (dtype != CNNITMO_BF16 && !f32) return 0;
+  return halo_handles(a, f32) ? 1 : 0;
+}
+
 extern "C" int cnnitmo_conv3x3_fwd_cat(int dtype, const void* x1, int x1_ld, int x1_off, int c1, const void* x2,
                                        int x2_ld, int x2_off, int n, int h, int w, int cin, const void* wt,
                                        const float* bias, int cout, void* out, int out_ld, int out_off, int flags,

@@ -147,6 +147,7 @@ class BlockStage(Stage):
     def __init__(self, kind, conv, relu, bn, drop, drop_id, vin, vout):
         self.kind, self.conv, self.relu, self.bn, self.drop = kind, conv, relu, bn, drop
         self.pool = None  # the PoolStage whose 2x2 max-pool this conv's epilogue computes (Engine._plan_pool_fusion)
+        self.head = None  # the HeadStage this conv's inference epilogue computes (Engine._plan_head_fusion)
         self.drop_id = drop_id
         self.vin, self.vout = vin, vout
         self.cin = vin.c if kind != "c3in" else 3
@@ -245,6 +246,19 @@ class BlockStage(Stage):
         else:
             ops.tconv_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
 
+    def _conv_head(self, n):
+        """predict(): this conv with the sigmoid head in its epilogue, straight into the
+        prediction buffer (cnnitmo_conv3x3_fwd_head); the conv's own output is never stored."""
+        e, bn, cout = self.eng, self.bn, self.cout
+        sc = torch.empty(cout, device=e.device, dtype=torch.float32)
+        sh = torch.empty(cout, device=e.device, dtype=torch.float32)
+        ops.bn_infer_coeffs(cout, e.p(bn.name + "/gamma"), e.p(bn.name + "/beta"), e.b(bn.name + "/moving_mean"),
+                            e.b(bn.name + "/moving_variance"), bn.epsilon, sc, sh)
+        hd = self.head
+        ops.conv3x3_fwd_head(e.dt, self.vin.view(n), self.w_fwd, e.p(self.conv.name + "/bias"), cout,
+                             (L.RELU if self.relu else 0) | L.AFFINE, (sc, sh), e.h_valid, e.p(hd.name + "/kernel"),
+                             e.p(hd.name + "/bias"), e._yhat)
+
     def _pool_bufs(self, n):
         """(pooled output, window indices, pool sign) for the fused MaxPooling2D: in training
         the epilogue stores r with the BN folded into the consumers, so it pools r by the
@@ -278,6 +292,9 @@ class BlockStage(Stage):
         P = n * self.vout.h * self.vout.w
         self.fold_active = training and self.foldable
         self.direct = self.direct_ok
+        if not training and self.head is not None and e._yhat is not None:
+            self._conv_head(n)
+            return
         if self.kind == "c3in" and not self.direct:
             self.cols = torch.empty(P * 32, dtype=e.tdtype, device=e.device)
             ops.im2col_c3(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, self.cols)
@@ -622,8 +639,12 @@ class HeadStage(Stage):
         self.cin = vin.c
         self.params = [(layer.name + "/kernel", (3, 1, 1, self.cin)), (layer.name + "/bias", (3,))]
 
+    fused = False  # computed by its producer's epilogue in predict() (Engine._plan_head_fusion)
+
     def infer(self, n, yhat):
         e = self.eng
+        if self.fused:
+            return  # (written by the producer's cnnitmo_conv3x3_fwd_head)
         ops.head_fwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
                      e.p(self.name + "/bias"), yhat)
 
@@ -834,6 +855,8 @@ class Engine:
         self.stages = compile_graph(model, fold=os.environ.get("CNNITMO_NO_FOLD", "0") != "1")
         self._plan_split_concats()
         self._plan_pool_fusion()
+        self._plan_head_fusion()
+        self._yhat = None
         self.training = False
         self.h_valid = None
         self.update_moving = True
@@ -917,6 +940,29 @@ class Engine:
             prod.pool = st
             st.vout.folded = True
             st.vout.coef_src = v
+
+    def _plan_head_fusion(self):
+        """The sigmoid head (model.py:264) into the inference epilogue of the 3x3 ConvBN that
+        feeds it (conv9's second conv): predict() then never stores that conv's 64-channel
+        output (fp32 b8 at 1080p: 4.3 GB written and read back).  Needs: a 'c3' producer with
+        BN and no Dropout / pooling / concat, consumed by the head alone, 64 channels, the halo
+        kernel for its sizes.  CNNITMO_HEAD_FUSE=0: the stand-alone head kernel."""
+        if os.environ.get("CNNITMO_HEAD_FUSE", "1") == "0":
+            return
+        head = self.stages[-1]
+        if not isinstance(head, HeadStage):
+            return
+        v = head.vin
+        prod = v.producer
+        readers = sum(1 for st in self.stages if getattr(st, "vin", None) is v or v in getattr(st, "vins", []))
+        if (prod is None or not isinstance(prod, BlockStage) or prod.kind != "c3" or prod.bn is None
+                or prod.drop is not None or prod.pool is not None or v.place or v.split or prod.vin.split
+                or readers != 1 or prod.cout != 64 or head.cin != 64):
+            return
+        if not ops.head_supported(self.dt, 1, v.h, v.w, prod.cin, prod.cout):
+            return
+        prod.head = head
+        head.fused = True
 
     # ---- parameter access ---------------------------------------------------
     def _slice(self, flat, table, key):
@@ -1012,8 +1058,15 @@ class Engine:
         return n
 
     def predict(self, x):
-        n = self.forward(x, training=False)
-        yhat = torch.empty(n, self.h_valid, self.model.inputs[0].shape[1], 3, device=self.device, dtype=torch.float32)
+        # [n, h_valid, w, 3]: x's valid rows (forward's _input); a fused head writes it from
+        # its producer's epilogue during the forward
+        yhat = torch.empty(x.shape[0], x.shape[1], self.model.inputs[0].shape[1], 3, device=self.device,
+                           dtype=torch.float32)
+        self._yhat = yhat
+        try:
+            n = self.forward(x, training=False)
+        finally:
+            self._yhat = None
         self.stages[-1].infer(n, yhat)
         self._release()
         return yhat

@@ -80,6 +80,18 @@ def pool_supported(dt, n, h, w, cin, cout):
     return query("cnnitmo_conv3x3_pool_supported", dt, n, h, w, cin, cout) == 1
 
 
+def conv3x3_fwd_head(dt, x: View, wt, bias, cout, flags, aff, h_valid, head_w, head_b, yhat):
+    """The inference forward of the last 3x3 ConvBN with the sigmoid head in its epilogue
+    (cnnitmo_conv3x3_fwd_head): yhat [n, h_valid, w, 3] fp32; the conv output is not stored."""
+    sc, sh = aff if aff is not None else (None, None)
+    call("cnnitmo_conv3x3_fwd_head", dt, x.ptr, x.ld, x.off, x.n, x.h, x.w, x.c, ptr(wt), ptr(bias), cout, flags,
+         ptr(sc), ptr(sh), h_valid, ptr(head_w), ptr(head_b), ptr(yhat), stream_ptr())
+
+
+def head_supported(dt, n, h, w, cin, cout):
+    return query("cnnitmo_conv3x3_head_supported", dt, n, h, w, cin, cout) == 1
+
+
 def conv3x3_fwd_cat(dt, x1: View, x2: View, wt, bias, out: View, flags=0, aff=None, stats=None, border=None):
     """conv3x3_fwd over concatenate([x1, x2]) read from its members (cnnitmo_conv3x3_fwd_cat)."""
     sc, sh = aff if aff is not None else (None, None)

@@ -89,6 +89,16 @@ int cnnitmo_conv3x3_fwd_pool(int dtype, const void* x, int x_ld, int x_off, int 
                              int flags, const float* aff_scale, const float* aff_shift, float* stat_part,
                              const float* border, void* pool_out, int pool_ld, unsigned char* pool_idx,
                              const float* pool_sign, void* stream);
+/* The last 3x3 ConvBN (model.py:262-263, conv9's second conv) with the sigmoid head
+ * (model.py:264, Conv2D(3, 1, activation='sigmoid')) in its epilogue, for inference
+ * (predict.py:62): yhat [n][h_valid][w][3] fp32 = sigmoid(y . head_w[3][cout] + head_b), y = the
+ * conv's epilogue output (flags/aff as cnnitmo_conv3x3_fwd: ReLU, BN affine), never stored.
+ * Replaces cnnitmo_conv3x3_fwd + cnnitmo_head_fwd.  cout = 64; no BN sums. */
+int cnnitmo_conv3x3_fwd_head(int dtype, const void* x, int x_ld, int x_off, int n, int h, int w, int cin,
+                             const void* wt, const float* bias, int cout, int flags, const float* aff_scale,
+                             const float* aff_shift, int h_valid, const float* head_w, const float* head_b,
+                             float* yhat, void* stream);
+int cnnitmo_conv3x3_head_supported(int dtype, int n, int h, int w, int cin, int cout);
 int cnnitmo_conv3x3_pool_supported(int dtype, int n, int h, int w, int cin, int cout);
 
 /* conv3x3_fwd over concatenate([x1, x2]) (model.py:261, Keras axis=3) read from its

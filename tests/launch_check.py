@@ -126,7 +126,7 @@ class _Acc:
 
 
 # every launching entry point of cnn_itmo_amd.ops (all of them go through ops.call)
-LAUNCHES = ("conv3x3_fwd", "conv3x3_fwd_pool", "pool_bnsums_pooled", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
+LAUNCHES = ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_head", "pool_bnsums_pooled", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
             "conv_wgrad", "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad", "conv1tap_fwd", "im2col_c3",
             "maxpool_fwd", "maxpool_bwd", "pool_bnsums", "bn_fwd_finalize", "bn_infer_coeffs", "bn_apply",
             "bn_bwd_reduce", "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3",
@@ -240,6 +240,24 @@ class LaunchChecker(ElementwiseChecks):
         self._chk_conv3x3_fwd(dt, x, wt, bias, out, flags, aff, stats, border, tag="_pool")
         self._chk_pool_of_stored(f"conv3x3_fwd_pool {x.n}x{x.h}x{x.w} {x.c}->{out.c}", dt, out, pool_out, pool_idx,
                                  pool_sign)
+
+    def _chk_conv3x3_fwd_head(self, dt, x, wt, bias, cout, flags, aff, h_valid, head_w, head_b, yhat):
+        """yhat = sigmoid(epilogue(conv) . head_w^T + head_b) over the valid rows; the conv is
+        accumulated in fp32 from operands in dtype and never rounded to dtype, so the bound is
+        the fp32 accumulation slack carried through the head's weights, plus the head's own
+        fp32 dot product, times the sigmoid's slope (<= 1/4)."""
+        n, h, w, cin = x.n, x.h, x.w, x.c
+        lab = f"conv3x3_fwd_head {n}x{h}x{w} {cin}->{cout}->3 (valid {h_valid})"
+        W = wt.view(cout, 3, 3, cin)
+        Hw, hb = head_w.view(3, cout).to(F64), head_b.to(F64)
+        yt, xt = yhat.view(n, h_valid, w, 3), x.tensor()
+        sc = aff[0].to(F64).abs() if (flags & L.AFFINE) else 1.0
+        for i in range(n):
+            y = _epilogue(_conv3(xt[i], W) + bias.to(F64), flags, aff)[:h_valid]
+            sl = (_f32_slack(L.F32, 9 * cin, _conv3(xt[i].abs(), W.abs())) * sc)[:h_valid]
+            z = y @ Hw.t() + hb
+            dz = sl @ Hw.abs().t() + 16 * 2.0 ** -24 * (y.abs() @ Hw.abs().t() + hb.abs())
+            self._close(lab, yt[i], torch.sigmoid(z), 0.25 * dz + 1e-7)
 
     @staticmethod
     def _cat_view(x1, x2):

@@ -459,6 +459,40 @@ def test_conv3x3_fwd_pool(dt, cin, cout, H, W):
         assert torch.equal(pv.view(N, H // 2, W // 2, cout), y.gather(3, first.unsqueeze(3)).squeeze(3))
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("cin,H,W,hv", [(64, 18, 70, 17), (96, 16, 64, 16), (64, 5, 33, 3)])
+def test_conv3x3_fwd_head(dt, cin, H, W, hv):
+    """cnnitmo_conv3x3_fwd_head (model.py:262-264 in predict): conv3x3 + ReLU + the inference
+    BN affine + the 1x1 sigmoid head, the conv output never stored, vs the fp64 oracle on
+    operands rounded to dtype (the conv accumulates in fp32 and is not rounded to dtype).
+    Partial tiles, valid rows < h."""
+    from cnn_itmo_amd import ops
+    from cnn_itmo_amd import _lib as L
+    rng = np.random.default_rng(cin + H + hv)
+    N, cout = 2, 64
+    x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
+    w = (rng.standard_normal((cout, 3, 3, cin)) * 0.05).astype(np.float32)
+    b = (rng.standard_normal(cout) * 0.1).astype(np.float32)
+    s, h = rng.uniform(0.5, 1.5, cout).astype(np.float32), rng.normal(0, 0.2, cout).astype(np.float32)
+    hw = (rng.standard_normal((3, cout)) * 0.2).astype(np.float32)
+    hb = rng.standard_normal(3).astype(np.float32)
+    d, T = DT[dt], TDT[dt]
+    if not ops.head_supported(d, N, H, W, cin, cout):
+        pytest.skip("halo kernel does not take this shape")
+    wf = torch.empty(w.size, dtype=T, device="cuda")
+    ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cin, wf, None)
+    xv = ops.View(dev(x, dt).reshape(-1), N, H, W, cin, cin)
+    yhat = torch.full((N, hv, W, 3), -1.0, device="cuda")
+    ops.conv3x3_fwd_head(d, xv, wf, torch.tensor(b).cuda(), cout, L.RELU | L.AFFINE,
+                         (torch.tensor(s).cuda(), torch.tensor(h).cuda()), hv, torch.tensor(hw).cuda(),
+                         torch.tensor(hb).cuda(), yhat)
+    torch.cuda.synchronize()
+    y = np.maximum(R.conv2d_same(rnd(x, dt), rnd(w, dt), b), 0) * s + h
+    z = y[:, :hv] @ hw.T.astype(np.float64) + hb
+    ref = 1.0 / (1.0 + np.exp(-z))
+    np.testing.assert_allclose(host(yhat), ref, rtol=0, atol=2e-5 if dt == "f32" else 5e-5)
+
+
 @pytest.mark.parametrize("H,W", [(16, 64), (20, 70), (8, 40)])
 @pytest.mark.parametrize("th8", ["1", "0"])
 def test_conv3x3_fwd_cat_dec9a(H, W, th8):
