@@ -408,6 +408,9 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // parity-green but neutral on enc2b/dec6/dec8/dec9 (profiles/r03z_ab_halo_lines.txt;
   // the halo conv's stores are a small share of its time), so off by default.
   constexpr bool LINES = HALO_LINES && FP == 2 && ES == 2;
+  // the pooled training forward stores r with the BN folded into its consumers: no affine
+  // epilogue (halo_plan), which keeps the bf16 BN-64 kernel from spilling
+  constexpr bool AFFOK = !(POOL && !NOSUM);
   auto epilogue = [&](const Pos& e) {
     const int oh0 = e.y0 + wave * RPW;
     const TE* obase = (const TE*)p.out + (((size_t)e.img * p.ho + oh0) * p.wo + e.x0) * p.out_ld + p.out_off + n0;
@@ -435,8 +438,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       float bj[8], sj[8], hj[8], md[8], hw[EPI == 3 ? 3 : 1][8];
       if constexpr (EPI == 1 || EPI == 3) {
         lds8(par + cl, bj);
-        lds8(par + BN + cl, sj);
-        lds8(par + 2 * BN + cl, hj);
+        if constexpr (AFFOK) {
+          lds8(par + BN + cl, sj);
+          lds8(par + 2 * BN + cl, hj);
+        }
       }
       if constexpr (EPI == 3) {
 #pragma unroll
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k], 0.f);
           }
-          if (aff) {
+          if (AFFOK && aff) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] = fmaf(v[k], sj[k], hj[k]);
           }
@@ -965,6 +970,8 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   if (a.ntaps != 9 || a.scale != 1 || a.scatter || a.hs != a.ho || a.ws != a.wo) return false;
   if (a.pool_out && (a.a2 || a.bnb_out || a.ho % 2 || a.wo % 2 || a.pool_ld % 8 || a.pool_ld < a.N || !a.pool_idx))
     return false;
+  // pooled forward: BN sums (training, BN folded: r stored) or the affine (inference), not both
+  if (a.pool_out && (a.flags & CNNITMO_STATS) && (a.flags & CNNITMO_AFFINE)) return false;
   pl.bn = a.N % 64 == 0 ? 64 : (a.N % 32 == 0 ? 32 : 0);
   if (!pl.bn || a.N / pl.bn > halo_ncu() / 8) return false;
   if (a.bnb_out) {  // fused BN backward (input gradient)
