@@ -376,3 +376,33 @@ def test_fused_pool_checks(dt):
     part = torch.stack([gd.sum(0), (gd * (pd - mean.double()) * inv.double()).sum(0)]).float()[None]
     chk._chk_pool_bnsums_pooled(dt, dyp, pv, n, h, w, c, mean, inv, part)
     _fails(chk._chk_pool_bnsums_pooled, dt, dyp, pv, n, h, w, c, mean, inv, _bump(part, i=c + 2, by=1.0))
+
+
+@pytest.mark.parametrize("dt", [L.BF16, L.F32])
+def test_fused_head_check(dt):
+    """cnnitmo_conv3x3_fwd_head's check: an fp32 evaluation of the contract (3x3 conv in fp32
+    from dtype operands, ReLU, BN affine, the 1x1 head, sigmoid) passes; a value off by more
+    than the fp32 slack fails, and so does a prediction of the unrounded conv with the affine
+    left out."""
+    T = BF if dt == L.BF16 else F32
+    g = torch.Generator().manual_seed(5)
+    n, h, w, cin, cout, hv = 2, 5, 7, 16, 64, 4
+    x = torch.randn(n * h * w * cin, generator=g).to(T)
+    wt = (torch.randn(cout * 9 * cin, generator=g) * 0.1).to(T)
+    bias = torch.randn(cout, generator=g) * 0.1
+    sc, sh = torch.rand(cout, generator=g) + 0.5, torch.randn(cout, generator=g) * 0.1
+    hw, hb = torch.randn(3 * cout, generator=g) * 0.2, torch.randn(3, generator=g)
+    xv = View(x, n, h, w, cin, cin)
+    # fp32 evaluation: conv over fp32 operands, then the epilogue and the head in fp32
+    xf = x.float().view(n, h, w, cin).permute(0, 3, 1, 2)
+    wf = wt.float().view(cout, 3, 3, cin).permute(0, 3, 1, 2)
+    z = torch.nn.functional.conv2d(xf, wf, bias, padding=1).permute(0, 2, 3, 1)
+    y = torch.relu(z) * sc + sh
+    yh = torch.sigmoid(y[:, :hv] @ hw.view(3, cout).t() + hb).contiguous()
+    chk = _checker(dt)
+    flags = L.RELU | L.AFFINE
+    chk._chk_conv3x3_fwd_head(dt, xv, wt, bias, cout, flags, (sc, sh), hv, hw, hb, yh.view(-1))
+    _fails(chk._chk_conv3x3_fwd_head, dt, xv, wt, bias, cout, flags, (sc, sh), hv, hw, hb, _bump(yh.view(-1), by=1e-3))
+    y2 = torch.relu(z)
+    yh2 = torch.sigmoid(y2[:, :hv] @ hw.view(3, cout).t() + hb).contiguous()
+    _fails(chk._chk_conv3x3_fwd_head, dt, xv, wt, bias, cout, flags, (sc, sh), hv, hw, hb, yh2.view(-1))
