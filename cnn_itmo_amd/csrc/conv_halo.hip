@@ -263,13 +263,11 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     boff[i] = row < KT * BN ? (unsigned)((pair_perm(nn) * K + tap * p.cin + piece * PE) * ES) : OOB;
   }
   uintptr_t pbase = 0, bbase = 0;
-  // LDS addresses as 32-bit integers (the DMA's M0): the stage being filled and the kernel's base
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane(dma::lds_addr(smem));
-  unsigned iPa = lds0;
+  char* iPs = smem;
   unsigned pvo[NPI];
   auto issue_prep = [&](int buf) {
     const Pos& s = ip;
-    iPa = lds0 + buf * STAGE;
+    iPs = smem + buf * STAGE;
     const long po = ((long)s.img * p.hs + s.y0 - 1) * p.ws + s.x0 - 1;  // patch origin pixel (may be < 0)
     const int c = s.ch * CC;
     bbase = (uintptr_t)(Wt + (size_t)n0 * K + c);
@@ -297,10 +295,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   auto issue_piece = [&](int k) {  // k: compile-time after unrolling
     if (k < NPI) {
       const int gp = wave * NPI + k;
-      dma::lds16a(pvo[k], dma::rsrc(pbase), gp < PPC ? iPa + gp * 1024 : lds0 + C::SCR);
+      dma::lds16(pvo[k], dma::rsrc(pbase), gp < PPC ? iPs + gp * 1024 : smem + C::SCR);
     } else if constexpr (!RES) {
       const int gp = wave * NBI + (k - NPI);
-      dma::lds16a(boff[k - NPI], dma::rsrc(bbase), gp < C::BPC ? iPa + C::PATCH + gp * 1024 : lds0 + C::SCR);
+      dma::lds16(boff[k - NPI], dma::rsrc(bbase), gp < C::BPC ? iPs + C::PATCH + gp * 1024 : smem + C::SCR);
     }
   };
 

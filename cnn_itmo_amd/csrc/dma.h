@@ -35,13 +35,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)u, (short)0, 0x7FFFFFF0, 0x00020000);
 }
 
-// the same with the destination as a 32-bit LDS address (wave-uniform): no generic-pointer
-// cast, whose null check costs a 64-bit compare and a select per instruction
-__device__ __forceinline__ void lds16a(unsigned voff, i32x4 rs, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs),
-               "s"(lds) : "memory");
-}
-
 // one 16-byte piece per lane -> the wave's 1 KiB LDS image at `lds` (LDS-DMA,
 // lane-linear destination)
 __device__ __forceinline__ void lds16(unsigned voff, i32x4 rs, const char* lds) {
