@@ -32,6 +32,7 @@ import functools
 import io
 import json
 import os
+import re
 import sys
 import time
 
@@ -117,7 +118,7 @@ class KernelTimer:
     def _wrap(self):
         ops = self.ops
         query = functools.lru_cache(maxsize=None)(ops.query)  # kernel names: one ctypes query per shape
-        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
+        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_head", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
                                            "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
                                            "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad")}
 
@@ -139,6 +140,14 @@ class KernelTimer:
             nm = kname(dt, x.n, x.h, x.w, x.c, out.c, 0).replace(">", ",pool>")
             return self._bracket(nm, fl, f"fwd+pool {x.h}x{x.w} {x.c}->{out.c}", o["conv3x3_fwd_pool"], dt, x, wt,
                                  bias, out, *a, **k)
+
+        def conv3x3_fwd_head(dt, x, wt, bias, cout, flags, aff, h_valid, head_w, head_b, yhat):
+            # the conv's FLOPs + the 1x1 cout->3 head; bytes: input, weights and the fp32 yhat
+            fl = 2.0 * x.p * cout * 9 * x.c + 2.0 * x.n * h_valid * x.w * 3 * cout
+            self._nb = (2 if dt == 1 else 4) * (x.p * x.c + 9 * x.c * cout) + 4 * 3 * x.n * h_valid * x.w
+            nm = re.sub(r",1([,>])", r",3\1", kname(dt, x.n, x.h, x.w, x.c, cout, 0), count=1)
+            return self._bracket(nm, fl, f"fwd+head {x.h}x{x.w} {x.c}->{cout}->3", o["conv3x3_fwd_head"], dt, x, wt,
+                                 bias, cout, flags, aff, h_valid, head_w, head_b, yhat)
 
         def conv3x3_fwd_cat(dt, x1, x2, wt, bias, out, *a, **k):
             cin = x1.c + x2.c
@@ -214,6 +223,7 @@ class KernelTimer:
                                  dt, x, dout, cout, dk, *a, **k)
 
         for n, f in (("conv3x3_fwd", conv3x3_fwd), ("conv3x3_fwd_pool", conv3x3_fwd_pool),
+                     ("conv3x3_fwd_head", conv3x3_fwd_head),
                      ("conv3x3_fwd_cat", conv3x3_fwd_cat), ("conv_wgrad_cat", conv_wgrad_cat),
                      ("conv3x3_dgrad", conv3x3_dgrad),
                      ("conv3x3_dgrad_bn", conv3x3_dgrad_bn), ("tconv_fwd", tconv_fwd),
