@@ -461,10 +461,8 @@ def main():
 
     def step(i):
         if args.mode == "infer":
-            eng.forward(x, training=False)
             yhat = torch.empty(B, args.height, args.width, 3, device="cuda", dtype=torch.float32)
-            eng.stages[-1].infer(B, yhat)
-            eng._release()
+            eng.predict_into(x, yhat)  # Model.predict's path (fused head included)
             return None
         kw = dict(seed=i * world + rank, lr=opt.lr, rho=opt.rho, eps=opt.epsilon)
         if dp is not None:
@@ -657,9 +655,7 @@ def infer_leg(args, rank, world, timer, barrier, agree, P_init, H, W, B, with_cp
         agree(ok)
 
     def step():
-        eng.forward(x, training=False)
-        eng.stages[-1].infer(B, yhat)
-        eng._release()
+        eng.predict_into(x, yhat)  # Model.predict's path: the head is computed every step
 
     def timed(n):
         barrier()

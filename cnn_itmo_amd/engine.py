@@ -147,6 +147,7 @@ class BlockStage(Stage):
     def __init__(self, kind, conv, relu, bn, drop, drop_id, vin, vout):
         self.kind, self.conv, self.relu, self.bn, self.drop = kind, conv, relu, bn, drop
         self.pool = None  # the PoolStage whose 2x2 max-pool this conv's epilogue computes (Engine._plan_pool_fusion)
+        self.head_ran = False  # this forward computed the head (predict with a fused head)
         self.head = None  # the HeadStage this conv's inference epilogue computes (Engine._plan_head_fusion)
         self.drop_id = drop_id
         self.vin, self.vout = vin, vout
@@ -292,8 +293,10 @@ class BlockStage(Stage):
         P = n * self.vout.h * self.vout.w
         self.fold_active = training and self.foldable
         self.direct = self.direct_ok
+        self.head_ran = False
         if not training and self.head is not None and e._yhat is not None:
             self._conv_head(n)
+            self.head_ran = True
             return
         if self.kind == "c3in" and not self.direct:
             self.cols = torch.empty(P * 32, dtype=e.tdtype, device=e.device)
@@ -643,8 +646,8 @@ class HeadStage(Stage):
 
     def infer(self, n, yhat):
         e = self.eng
-        if self.fused:
-            return  # (written by the producer's cnnitmo_conv3x3_fwd_head)
+        if self.fused and self.vin.producer.head_ran:
+            return  # (written by the producer's cnnitmo_conv3x3_fwd_head in this forward)
         ops.head_fwd(e.dt, self.vin.view(n), e.h_valid, e.p(self.name + "/kernel"),
                      e.p(self.name + "/bias"), yhat)
 
@@ -1058,10 +1061,18 @@ class Engine:
         return n
 
     def predict(self, x):
-        # [n, h_valid, w, 3]: x's valid rows (forward's _input); a fused head writes it from
-        # its producer's epilogue during the forward
+        # [n, h_valid, w, 3]: x's valid rows (forward's _input)
         yhat = torch.empty(x.shape[0], x.shape[1], self.model.inputs[0].shape[1], 3, device=self.device,
                            dtype=torch.float32)
+        return self.predict_into(x, yhat)
+
+    def predict_into(self, x, yhat):
+        """predict() into a caller's fp32 [n, h_valid, w, 3] buffer (bench.py's inference legs
+        reuse one).  A fused head writes it from its producer's epilogue during the forward."""
+        if tuple(yhat.shape) != (x.shape[0], x.shape[1], self.model.inputs[0].shape[1], 3) or \
+                yhat.dtype != torch.float32 or not yhat.is_contiguous():
+            raise ValueError(f"predict_into: yhat must be contiguous fp32 {(x.shape[0], x.shape[1])} x W x 3, "
+                             f"got {tuple(yhat.shape)} {yhat.dtype}")
         self._yhat = yhat
         try:
             n = self.forward(x, training=False)

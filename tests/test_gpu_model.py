@@ -82,6 +82,39 @@ def test_unet_inference_parity(dtype):
         assert err <= 3e-2, err
 
 
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_fused_head_paths_agree(dtype):
+    """The head is computed on every inference path: predict / predict_into (head fused into
+    conv9's epilogue, engine.py _plan_head_fusion) and a bare forward + HeadStage.infer (the
+    stand-alone head kernel, since no fused head ran in that forward) give the same frames."""
+    rng = np.random.default_rng(4)
+    m = build_unet((64, 96, 3), dtype)
+    P = randomize_bn(m, rng)
+    e = m._engine()
+    assert e.stages[-1].fused, "the head-fusion plan should apply to the U-Net"
+    x = torch.tensor(rng.integers(0, 256, size=(2, 64, 96, 3)) / 255.0, dtype=torch.float32).cuda()
+    y_fused = torch.full((2, 64, 96, 3), -1.0, device="cuda")
+    e.predict_into(x, y_fused)
+    assert e.stages[-1].vin.producer.head_ran
+    y_plain = torch.full((2, 64, 96, 3), -1.0, device="cuda")
+    n = e.forward(x, training=False)
+    assert not e.stages[-1].vin.producer.head_ran
+    e.stages[-1].infer(n, y_plain)
+    e._release()
+    torch.cuda.synchronize()
+    a, b = y_fused.cpu().numpy(), y_plain.cpu().numpy()
+    assert a.min() >= 0.0 and b.min() >= 0.0  # every value written (the -1 fill is gone)
+    ref = R.UNetRef(P).forward(x.cpu().numpy().astype(np.float64), training=False)
+    tol = 1e-4 if dtype == "float32" else 3e-2
+    assert float(np.abs(a - ref).max()) <= tol
+    assert float(np.abs(b - ref).max()) <= tol
+    # the two heads differ only by the summation order of the 64-channel dot product
+    # (fp32) or by the bf16 rounding of the stored conv output (bf16)
+    assert float(np.abs(a - b).max()) <= (1e-5 if dtype == "float32" else 3e-2)
+    with pytest.raises(ValueError):
+        e.predict_into(x, torch.empty((2, 64, 96, 4), device="cuda"))
+
+
 def test_unet_inference_padded_1080_style():
     """H not divisible by 16: pad=True model, zero-padded rows, cropped output."""
     import cnn_itmo_amd as C
