@@ -319,10 +319,25 @@ template <int C> __device__ __forceinline__ int ffo(int row, int col) {
   return row * (C * 4) + ((((col >> 4) ^ (row & 1))) << 6) + ((col & 15) << 2);
 }
 
+// row groups issued ahead for the fp32 64 x 32 block (enc2a): with D = 2 its 102 KB ring
+// allows one 6-wave workgroup per CU; D = 1 (77 KB) two (dec9 on this block: 18.03 -> 17.45
+// ms, profiles/r04z_wf_layers.txt).  The 64 x 96 block (dec9, cin 96: one workgroup reads
+// each dz row once for all 96 input channels, 12 waves of 32 x 48 tiles, 144 VGPRs) fits
+// only with D = 1 (157 KB): dec9's fp32 weight gradient 17.93 -> 12.58 ms (103 -> 147 TF/s,
+// 0.93 of fp32 peak), fp32 training 30.96 -> 31.63 frames/s (profiles/r04z_wf96_*).
+#ifndef WF_D6432
+#define WF_D6432 1
+#endif
+#ifndef WF_BN96
+#define WF_BN96 1
+#endif
+constexpr int wf_ahead(int bm, int bn) { return bn == 96 ? 1 : (bm == 64 && bn == 32 ? WF_D6432 : 2); }
+constexpr int wf_wn(int bn) { return bn == 96 ? 2 : bn / 32; }  // waves across the BN columns
+
 template <int BM, int BN>
 struct WF32Cfg {
-  static constexpr int WM = BM / 32, WN = BN / 32, NWG = WM * WN, NW = 3 * NWG, NT = NW * 64;
-  static constexpr int TW = 64, XROWS = TW + 2, D = 2, R = 1;
+  static constexpr int WM = BM / 32, WN = wf_wn(BN), NWG = WM * WN, NW = 3 * NWG, NT = NW * 64;
+  static constexpr int TW = 64, XROWS = TW + 2, D = wf_ahead(BM, BN), R = 1;
   static constexpr int XB = (XROWS * BN * 4 + 1023) / 1024, DB = TW * BM * 4 / 1024;
   static constexpr int XS = D + R + 2, DS = D + R;
   static constexpr int SMEM = ((XS + 1) * XB + DS * DB) * 1024;
@@ -331,11 +346,11 @@ struct WF32Cfg {
 };
 
 template <int BM, int BN>
-__global__ __launch_bounds__(3 * (BM / 32) * (BN / 32) * 64) void wgrad_halo_f32_kernel(const WHArgs p) {
+__global__ __launch_bounds__(3 * (BM / 32) * wf_wn(BN) * 64) void wgrad_halo_f32_kernel(const WHArgs p) {
   using C = WF32Cfg<BM, BN>;
   constexpr int NW = C::NW, TW = C::TW, XB = C::XB, DB = C::DB, XS = C::XS, DS = C::DS, LX = C::LX, LD = C::LD;
   constexpr int D = C::D, WN = C::WN;
-  constexpr int FM = 2, FN = 2;  // 32 x 32 wave tiles
+  constexpr int FM = 2, FN = BN / (16 * WN);  // 32 x 32 (32 x 48 for BN 96) wave tiles
   __shared__ __attribute__((aligned(1024))) char smem[C::SMEM];
   char* const xbase = smem;
   char* const zrow = smem + XS * XB * 1024;
@@ -470,7 +485,7 @@ __global__ __launch_bounds__(3 * (BM / 32) * (BN / 32) * 64) void wgrad_halo_f32
           uint4 bfr[FN];
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
-            const int col = wn * 32 + j * 16 + li;
+            const int col = wn * (FN * 16) + j * 16 + li;
             f32x4 v;
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = *reinterpret_cast<const float*>(Xs + ffo<BN>(kk * 16 + 4 * e + g + s2, col));
@@ -501,7 +516,7 @@ __global__ __launch_bounds__(3 * (BM / 32) * (BN / 32) * 64) void wgrad_halo_f32
         const int t = wr * 3 + s2;
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          O[(size_t)co * 9 * p.cin + t * p.cin + n0 + wn * 32 + j * 16 + li] = acc[s2][i][j][rr];
+          O[(size_t)co * 9 * p.cin + t * p.cin + n0 + wn * (FN * 16) + j * 16 + li] = acc[s2][i][j][rr];
       }
 }
 
@@ -658,7 +673,8 @@ void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
                      a);
 }
 
-// fp32 plan: 32 / 64 x 32 / 64 blocks, 64-pixel strips, the row split of wh_plan's policy
+// fp32 plan: 32 / 64 x 32 / 64 blocks (64 x 96 for cin 96), 64-pixel strips, the row split of
+// wh_plan's policy
 bool wh_plan_f32(int n, int h, int w, int cin, int cout, WHPlan& pl) {
   static const int mode = [] {
     const char* e = getenv("CNNITMO_WGRAD_HALO_F32");
@@ -667,6 +683,7 @@ bool wh_plan_f32(int n, int h, int w, int cin, int cout, WHPlan& pl) {
   if (!mode) return false;
   pl.bm = cout % 64 == 0 ? 64 : (cout % 32 == 0 ? 32 : 0);
   pl.bn = cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0);
+  if (WF_BN96 && pl.bm == 64 && cin % 96 == 0 && cin % 64 != 0) pl.bn = 96;
   if (!pl.bm || !pl.bn) return false;
   pl.tw = 64;
   pl.strips = (w + pl.tw - 1) / pl.tw;
@@ -683,7 +700,8 @@ bool wh_plan_f32(int n, int h, int w, int cin, int cout, WHPlan& pl) {
     if (ncu <= 0) ncu = 256;
   }
   const int xb = (66 * pl.bn * 4 + 1023) / 1024, db = 64 * pl.bm * 4 / 1024;
-  const int smem = (6 * xb + 3 * db) * 1024;  // WF32Cfg::SMEM
+  const int d = wf_ahead(pl.bm, pl.bn);
+  const int smem = ((d + 4) * xb + (d + 1) * db) * 1024;  // WF32Cfg::SMEM (R = 1)
   const long slots = (long)ncu * std::max(1, (160 * 1024) / smem);
   long best = 1;
   double best_eff = -1.0;
@@ -769,6 +787,9 @@ int launch_wgrad_halo_f32(const float* x, long x_ld, int x_off, const float* dz,
     return pl.strips * pl.rsplits;                                                                       \
   }
   WF(64, 64) WF(64, 32) WF(32, 64) WF(32, 32)
+#if WF_BN96
+  WF(64, 96)
+#endif
 #undef WF
   return -1;
 }
