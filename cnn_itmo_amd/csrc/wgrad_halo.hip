@@ -541,7 +541,9 @@ __global__ __launch_bounds__(3 * (BM / 32) * wf_wn(BN) * 64) void wgrad_halo_f32
 constexpr int wh_rows(int bm, int bn) {
   return bm == 64 && bn >= 96 ? WH_ROWS96 : (bm == 64 && bn == 64 ? WH_ROWS64 : WH_ROWS_SMALL);
 }
-// row groups issued ahead (64 x 128: two, the most that fits beside its 17 KB x rows)
+// row groups issued ahead (64 x 128: two, the most that fits beside its 17 KB x rows).  For
+// 64 x 96 two ahead is neutral (dec8 + dec9 11.38-11.40 vs 11.44-11.45 ms) and one row per
+// step with two ahead 6 % slower (profiles/r04zz_wh96_ring_ab.txt)
 #ifndef WH_AHEAD96
 #define WH_AHEAD96 3
 #endif
