@@ -105,6 +105,13 @@ def main():
             if "wgrad" in want:
                 dw = torch.empty(cout * 9 * cin, device="cuda", dtype=torch.float32)
                 rows.append((name, "wgrad", fl, timeit(lambda: ops.conv_wgrad(dt, 9, x, out.buf, cout, dw), a.iters)))
+            if "wgradcat" in want and cin == 96:  # dec9's [conv1 32 | up9 64] read from its two members
+                x1, x2 = ops.new_view(B, h, w, 32, T), ops.new_view(B, h, w, 64, T)
+                x1.buf.uniform_(-1, 1)
+                x2.buf.uniform_(-1, 1)
+                dw = torch.empty(cout * 9 * cin, device="cuda", dtype=torch.float32)
+                rows.append((name, "wgcat", fl, timeit(lambda: ops.conv_wgrad_cat(dt, x1, x2, out.buf, cout, dw), a.iters)))
+                del x1, x2
             del x, out
         torch.cuda.empty_cache()
     tot = sum(r[3] for r in rows)
