@@ -118,8 +118,8 @@ class KernelTimer:
     def _wrap(self):
         ops = self.ops
         query = functools.lru_cache(maxsize=None)(ops.query)  # kernel names: one ctypes query per shape
-        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_head", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd",
-                                           "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
+        o = {n: getattr(ops, n) for n in ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_head", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "conv3x3_dgrad_bn_pooled",
+                                           "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn", "conv1tap_fwd", "conv_wgrad",
                                            "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad")}
 
         def kname(dt, n, h, w, cin, cout, dgrad):
@@ -175,6 +175,12 @@ class KernelTimer:
             return self._bracket(name, fl, f"dgrad_bn {h}x{w} {cout}->{cin}[{c0}:{c1}]", o["conv3x3_dgrad_bn"], dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1,
                                  *a, **k)
 
+        def conv3x3_dgrad_bn_pooled(dt, dz, n, h, w, cout, wflip, cin, *a, **k):
+            fl = 2.0 * n * h * w * cin * 9 * cout
+            name = query("cnnitmo_conv3x3_dgrad_bn_pooled_kernel_name", dt, n, h, w, cout, cin).decode()
+            return self._bracket(name, fl, f"dgrad_bn+route {h}x{w} {cout}->{cin}", o["conv3x3_dgrad_bn_pooled"], dt, dz,
+                                 n, h, w, cout, wflip, cin, *a, **k)
+
         def tconv_dgrad_bn(dt, dout, n, h, w, cout, kT, cin, *a, **k):
             fl = 2.0 * n * h * w * cin * 4 * cout
             name = query("cnnitmo_tconv2x2_dgrad_bn_kernel_name", dt, n, h, w, cout, cin).decode()
@@ -226,7 +232,8 @@ class KernelTimer:
                      ("conv3x3_fwd_head", conv3x3_fwd_head),
                      ("conv3x3_fwd_cat", conv3x3_fwd_cat), ("conv_wgrad_cat", conv_wgrad_cat),
                      ("conv3x3_dgrad", conv3x3_dgrad),
-                     ("conv3x3_dgrad_bn", conv3x3_dgrad_bn), ("tconv_fwd", tconv_fwd),
+                     ("conv3x3_dgrad_bn", conv3x3_dgrad_bn), ("conv3x3_dgrad_bn_pooled", conv3x3_dgrad_bn_pooled),
+                     ("tconv_fwd", tconv_fwd),
                      ("tconv_dgrad", tconv_dgrad), ("tconv_dgrad_bn", tconv_dgrad_bn), ("conv1tap_fwd", conv1tap_fwd), ("conv_wgrad", conv_wgrad),
                      ("tconv_wgrad", tconv_wgrad), ("conv_c3_fwd", conv_c3_fwd), ("conv_c3_wgrad", conv_c3_wgrad)):
             setattr(ops, n, f)

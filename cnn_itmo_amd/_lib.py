@@ -61,6 +61,10 @@ SIGNATURES = {
     "cnnitmo_conv3x3_dgrad_bn_rows": (i64, [i32, i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_conv3x3_dgrad_bn": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, i32, i32, vp, vp, i32,
                                        i32, vp, vp, i32, vp]),
+    "cnnitmo_conv3x3_dgrad_bn_pooled_rows": (i64, [i32] * 6),
+    "cnnitmo_conv3x3_dgrad_bn_pooled": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, vp, i32, i32, vp, vp, vp,
+                                              vp, vp]),
+    "cnnitmo_conv3x3_dgrad_bn_pooled_kernel_name": (C.c_char_p, [i32] * 6),
     "cnnitmo_conv3x3_dgrad": (i32, [i32, vp, i32, i32, i32, i32, vp, i32, vp, i32, i32, vp]),
     "cnnitmo_wgrad_workspace_bytes": (sz, [i32, i32, i32, i32, i32, i32, i32]),
     "cnnitmo_conv_wgrad": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp, sz, vp]),

@@ -51,13 +51,12 @@ namespace {
 
 using dma::OOB;
 
-// 8 waves (2 per SIMD, 64 x BN wave tiles).  HALO_NWAVE=4 (1 per SIMD, 128 x BN wave
-// tiles, accumulators in AGPRs, 25 % fewer LDS fragment reads per MFMA) compiles and
-// measured 8-10 % slower on every layer: one wave per SIMD does not hide the latencies.
-#ifndef HALO_NWAVE
-#define HALO_NWAVE 8
-#endif
-constexpr int TH = 16, TW = 32, NWAVE = HALO_NWAVE, NT = NWAVE * 64;
+// 8 waves (2 per SIMD, 64 x BN wave tiles).  (Measured and removed: one wave per SIMD with
+// 128 x BN wave tiles and AGPR accumulators, 8-10 % slower on every layer; the fused dgrad's
+// r loads issued during the last tap with the sums in LDS slots, 15-20 % slower; whole-line
+// epilogue stores, neutral; 8-row tiles for dec9's forward with all weights resident, 2 %
+// slower)
+constexpr int TH = 16, TW = 32, NWAVE = 8, NT = NWAVE * 64;
 constexpr int RPW = TH / NWAVE, FMR = TW / 16, FM = RPW * FMR;  // tile rows / fragments per wave
 constexpr int KT = 9, PW = TW + 2, PROWS = (TH + 2) * PW;         // halo patch: 18 x 34 rows of 64 B
 constexpr int PPC = (PROWS + 15) / 16;                            // patch pieces (1 KiB = 16 rows)
@@ -65,32 +64,14 @@ constexpr int NPI = (PPC + NWAVE - 1) / NWAVE;                    // patch piece
 // taps over which the next item's DMA pieces are issued (3 and 8 measured no better,
 // profiles/r02l_ab_halo_knobs.txt)
 constexpr int PFT = 5;
-#ifndef HALO_LINES
-#define HALO_LINES 0
-#endif
-// tap offset of the DMA issue window for waves NWAVE/2.. (the second wave on each SIMD):
-// the two waves of a SIMD then issue their pieces in different taps
-// EPI 2 (bf16): issue the epilogue's r loads during the tile's last tap (1) or after its
-// MFMAs (0).  1 compiles without spills (sums in per-wave LDS slots, 240-255 VGPRs) and is
-// parity-green, but measured 15-20 % slower on every fused dgrad (dec6-dec9b 38.2 -> 44.9 ms,
-// profiles/r04e_rtap_ab.txt): the last tap's MFMAs do not cover an HBM load, and the slot
-// read-modify-writes and row reductions add LDS and VALU work to every tile.
-#ifndef HALO_RTAP
-#define HALO_RTAP 0
-#endif
-#ifndef HALO_PFT_OFF
-#define HALO_PFT_OFF 0
-#endif
 
 // RES: the workgroup's weights for the whole K (at most RCH chunks) stay resident in
 // LDS, loaded once per launch; a ring stage then holds the halo patch only.  For the
 // small-K layers (cin <= 64: level 1 and 2) the per-item weight pieces were half of
 // every stage's DMA.
 constexpr int RCH = 2;
-// THT: tile rows (16; 8 for dec9a's forward: 96 input channels with all three weight chunks
-// resident, which needs the smaller patch to fit two stages beside them)
 template <int BN, bool RES, int THT = 16> struct HCfg {
-  static constexpr int RCH = THT == 8 ? 3 : ::RCH;
+  static constexpr int RCH = ::RCH;
   static constexpr int PPC = ((THT + 2) * PW + 15) / 16, NPI = (PPC + NWAVE - 1) / NWAVE;
   static constexpr int FN = BN / 16, FP = FN / 2;        // fragments / 32-column pairs
   static constexpr int BPC = KT * BN / 16;               // weight pieces
@@ -142,6 +123,12 @@ struct HaloArgs {
 // and pools it by its maximum.
 // NOSUM (EPI 1): no BN partial sums (the inference forward): the 2 x FP x 8 accumulators live across
 // the whole launch otherwise
+// POOL (EPI 2): the deferred MaxPooling2D backward of the producer's output rides on the fused BN
+// backward (cnnitmo_conv3x3_dgrad_bn_pooled): every column is BN-fused, and the gradient the
+// dgrad computes (the concat skip path) is first increased by the pooled gradient routed to this
+// pixel by the window indices (pool_out = dy_pool, pool_idx; the pool's [n][ho/2][wo/2][N]).  A
+// wave's two tile rows are one row of 2x2 windows, so a lane's window position is
+// (tile row, pixel-column parity) and the pooled row it reads is shared by both rows.
 template <typename TE, int BN, int EPI, bool RES, bool POOL = false, int THT = 16, bool NOSUM = false>
 __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   using C = HCfg<BN, RES, THT>;
@@ -150,23 +137,17 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   static_assert(RPW >= 1, "a tile row per wave at least");
   constexpr int FN = C::FN, FP = C::FP, L = C::L, NBI = C::NBI, STAGE = C::STAGE, ST = C::ST;
   constexpr int ES = sizeof(TE), CC = 64 / ES, PE = 16 / ES;
-  static_assert(!POOL || (EPI == 1 && RPW % 2 == 0), "pooling: the forward epilogue, whole window rows per wave");
+  static_assert(!POOL || ((EPI == 1 || EPI == 2) && RPW == 2), "pooling: whole window rows per wave");
   // stores per wave per epilogue (+ POOL: a value and an index store per window row and column block)
   // (EPI 3: three 4-byte yhat stores per fragment instead of the output rows)
   constexpr int NST = EPI == 3 ? FM * 3
-                               : C::NST * (ES == 4 ? 2 : 1) + (POOL ? FP * (RPW / 2) * FMR * (ES == 4 ? 3 : 2) : 0);
-  // EPI 2 with HALO_RTAP: the dz parity sums live in per-wave LDS slots [NWAVE][4][BN] (over
-  // the border table, which EPI 2 does not use) instead of 32 registers
-  constexpr bool SLOT = HALO_RTAP && EPI == 2 && ES == 2;
-  constexpr int SMEM = SLOT ? C::UTB + NWAVE * 4 * BN * 4 : C::SMEM;
+                               : C::NST * (ES == 4 ? 2 : 1) + (POOL && EPI == 1 ? FP * (RPW / 2) * FMR * (ES == 4 ? 3 : 2) : 0);
+  constexpr int SMEM = C::SMEM;
   static_assert(SMEM <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   const FwdArgs& p = h.f;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the vmcnt switch
-#ifdef HALO_PRIO
-  if (wave >= NWAVE / 2) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half
-#endif
   // logical id: contiguous per XCD (xcd_remap), so a stream's workgroups share one
   // XCD's L2 except where a stream straddles two XCDs
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -203,8 +184,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       const int k = i / BN, c = n0 + i % BN;
       par[i] = (c >= p.bnb_c0 && c < p.bnb_c1) ? p.bnb_coef[k * cbn + c - p.bnb_c0] : 0.f;
     }
-    if constexpr (SLOT)
-      for (int i = tid; i < NWAVE * 4 * BN; i += NT) utb[i] = 0.f;
   }
 
   // item position: (image, tile row, tile column, chunk); tile rows fastest
@@ -336,19 +315,62 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const bool ok = e.y0 + wave * RPW + rr < p.ho && e.x0 + col < p.wo && c >= p.bnb_c0 && c < p.bnb_c1;
     return ok ? (unsigned)((((long)rr * p.wo + col) * p.bnb_r_ld + (c - p.bnb_c0)) * ES) : OOB;
   };
-  // EPI 2 (bf16, HALO_RTAP): r of the tile, loaded during the last item's last tap (whose
-  // next-tap fragment registers are free) instead of after its MFMAs
-  dma::i32x4 rvp[EPI == 2 && ES == 2 ? FM : 1][EPI == 2 && ES == 2 ? FP : 1];
-  auto load_r16 = [&](const Pos& e) {
-    if constexpr (EPI == 2 && ES == 2) {
-      const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
+  // EPI 2 + POOL: the pooled gradient and window indices of the lane's windows (both tile rows
+  // of a wave share one pooled row): [column block][pair], 8 channels each
+  constexpr int PRQ = POOL && EPI == 2 ? FMR : 1, PRP = POOL && EPI == 2 ? FP : 1;
+  dma::i32x4 gpv[PRQ][PRP][ES == 4 ? 2 : 1];
+  dma::i32x2 ipv[PRQ][PRP];
+  auto load_route = [&](const Pos& e) {
+    if constexpr (POOL && EPI == 2) {
+      const int ho2 = p.ho / 2, wo2 = p.wo / 2;
+      const size_t pb = (((size_t)e.img * ho2 + (e.y0 + wave * RPW) / 2) * wo2 + e.x0 / 2) * p.pool_ld + n0;
+      const __amdgpu_buffer_rsrc_t gs = dma::brsrc((const TE*)p.pool_out + pb);
+      const __amdgpu_buffer_rsrc_t is = dma::brsrc(p.pool_idx + pb);
+      const bool rok = e.y0 + wave * RPW < p.ho;
 #pragma unroll
-      for (int f = 0; f < FM; ++f)
+      for (int cb = 0; cb < FMR; ++cb)
 #pragma unroll
-        for (int q = 0; q < FP; ++q) rvp[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r_off(e, f, q), 0, 0);
+        for (int q = 0; q < FP; ++q) {
+          const bool ok = rok && e.x0 + cb * 16 + pxl < p.wo;
+          const unsigned o = (unsigned)((cb * 8 + (pxl >> 1)) * p.pool_ld + 32 * q + 8 * g);  // elements
+#pragma unroll
+          for (int h2 = 0; h2 < (ES == 4 ? 2 : 1); ++h2)
+            gpv[cb][q][h2] = __builtin_amdgcn_raw_buffer_load_b128(gs, ok ? o * ES + 16 * h2 : OOB, 0, 0);
+          ipv[cb][q] = __builtin_amdgcn_raw_buffer_load_b64(is, ok ? o : OOB, 0, 0);
+        }
     }
   };
-  auto compute = [&](int buf, bool pf, int ch, const Pos* rl = nullptr) {
+  // the routed pooled gradient of channels 8g..8g+7 of pair q for fragment f (window position
+  // (tile row, pixel-column parity)): added to the dgrad's value
+  auto routed = [&](int f, int q, float* gr) {
+    if constexpr (POOL && EPI == 2) {
+      const int rr = f / FMR, cb = f % FMR;
+      const unsigned k = (unsigned)(rr * 2 + (pxl & 1));
+      const unsigned i0 = (unsigned)ipv[cb][q][0], i1 = (unsigned)ipv[cb][q][1];
+      float gv[8];
+      if constexpr (ES == 2) {
+        const bf16x8 b8 = __builtin_bit_cast(bf16x8, gpv[cb][q][0]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gv[j] = to_f32(b8[j]);
+      } else {
+        const f32x4 a = __builtin_bit_cast(f32x4, gpv[cb][q][0]), b = __builtin_bit_cast(f32x4, gpv[cb][q][1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          gv[j] = a[j];
+          gv[4 + j] = b[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const unsigned ij = ((j < 4 ? i0 : i1) >> (8 * (j & 3))) & 0xFFu;
+        gr[j] = ij == k ? gv[j] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) gr[j] = 0.f;
+    }
+  };
+  auto compute = [&](int buf, bool pf, int ch) {
     const char* Ps = smem + buf * STAGE;
     const char* Bs = RES ? smem + C::WRES + ch * (C::BPC * 1024) : Ps + C::PATCH;
     uint4 af[2][FM], bfr[2][FN];
@@ -367,24 +389,22 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     for (int tap = 0; tap < KT; ++tap) {
       const int cur = tap & 1;
       if (tap + 1 < KT) load(tap + 1, cur ^ 1);
-      if (HALO_RTAP && tap == KT - 1 && rl) load_r16(*rl);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) Mma<TE>::run(acc[i][j], bfr[cur][j], af[cur][i]);  // C^T: lanes = pixels
       if (pf) {
-        const int toff = HALO_PFT_OFF && wave >= NWAVE / 2 ? HALO_PFT_OFF : 0;
 #pragma unroll
         for (int k = 0; k < L; ++k)
-          if ((k * PFT) / L + toff == tap) issue_piece(k);
+          if ((k * PFT) / L == tap) issue_piece(k);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
   // BN partial sums of the lane's pixels for its 8 channels of each pair (EPI 1), or
   // sums of dz by pixel-row parity (EPI 2; the lane's pixel-column parity is lane & 1)
-  constexpr int NSUM = EPI == 0 || EPI == 3 || SLOT || NOSUM ? 1 : FP;
+  constexpr int NSUM = EPI == 0 || EPI == 3 || NOSUM ? 1 : FP;
   float sa[NSUM][8], sb[NSUM][8];
 #pragma unroll
   for (int q = 0; q < NSUM; ++q)
@@ -402,12 +422,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     return __builtin_bit_cast(dma::i32x4, o);
   };
 
-  // EPI 0 / 1: stores through a buffer descriptor at the wave's first pixel.  HALO_LINES
-  // (BN 64): the two column pairs of a fragment go out as whole 128-byte lines, 8 pixels
-  // per store instruction (line_pair), instead of 16 pixels x 64 bytes per instruction:
-  // parity-green but neutral on enc2b/dec6/dec8/dec9 (profiles/r03z_ab_halo_lines.txt;
-  // the halo conv's stores are a small share of its time), so off by default.
-  constexpr bool LINES = HALO_LINES && FP == 2 && ES == 2;
+  // EPI 0 / 1: stores through a buffer descriptor at the wave's first pixel (whole 128-byte
+  // lines per store instruction measured neutral here: profiles/r03z_ab_halo_lines.txt)
   // the pooled training forward stores r with the BN folded into its consumers: no affine
   // epilogue (halo_plan), which keeps the bf16 BN-64 kernel from spilling
   constexpr bool AFFOK = !(POOL && !NOSUM);
@@ -417,8 +433,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const __amdgpu_buffer_rsrc_t os = dma::brsrc(obase);
     const bool relu = p.flags & CNNITMO_RELU, aff = p.flags & CNNITMO_AFFINE;
     const bool bt = EPI == 1 && p.border && (oh0 == 0 || oh0 + RPW >= p.ho || e.x0 == 0 || e.x0 + TW >= p.wo);
-    dma::i32x4 pk[LINES ? FP : 1][LINES ? FM : 1];
-    static_assert(!(LINES && POOL), "pooling stores from the fragment layout");
     // POOL: the wave's pooled rows start at (oh0 / 2, x0 / 2) of the [n][ho/2][wo/2] output
     const size_t pofs = (((size_t)e.img * (p.ho / 2) + oh0 / 2) * (p.wo / 2) + e.x0 / 2) * p.pool_ld + n0;
     const __amdgpu_buffer_rsrc_t ps = dma::brsrc(POOL ? (const TE*)p.pool_out + pofs : obase);
@@ -489,8 +503,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           for (int j = 0; j < 3; ++j)
 #pragma unroll
             for (int k = 0; k < 8; ++k) zf[f][j] = fmaf(v[k], hw[j][k], zf[f][j]);
-        } else if constexpr (LINES) {
-          pk[q][f] = pack8(v);
         } else if constexpr (ES == 4) {
           const unsigned off = (unsigned)((((long)rr * p.wo + col) * p.out_ld + cl) * 4);
           const float4 lo = {v[0], v[1], v[2], v[3]}, hi = {v[4], v[5], v[6], v[7]};
@@ -501,7 +513,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           pk8 = pack8(v);
           __builtin_amdgcn_raw_buffer_store_b128(pk8, os, ok ? off : OOB, 0, 0);
         }
-        if constexpr (POOL) {
+        if constexpr (POOL && EPI == 1) {
           // this window row as stored: the lane's pixel (tl) and its right neighbour (tr, DPP
           // quad_perm xor 1); a running maximum over the rows in window order (0,0), (0,1),
           // (1,0), (1,1), the first maximum winning (strict compares)
@@ -578,22 +590,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
         }
       }
     }
-    if constexpr (LINES) {
-#pragma unroll
-      for (int f = 0; f < FM; ++f) {
-        uint4 v1, v2;
-        line_pair(__builtin_bit_cast(uint4, pk[0][f]), __builtin_bit_cast(uint4, pk[1][f]), pxl, v1, v2);
-        const int rr = f / FMR, c1 = (f % FMR) * 16 + (pxl & 7), c2 = c1 + 8;
-        const int cl = 32 * (pxl >> 3) + 8 * g;
-        const bool rok = oh0 + rr < p.ho;
-        const unsigned o1 = (unsigned)((((long)rr * p.wo + c1) * p.out_ld + cl) * 2);
-        const unsigned o2 = (unsigned)((((long)rr * p.wo + c2) * p.out_ld + cl) * 2);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, v1), os,
-                                               rok && e.x0 + c1 < p.wo ? o1 : OOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, v2), os,
-                                               rok && e.x0 + c2 < p.wo ? o2 : OOB, 0, 0);
-      }
-    }
     zero_acc();
   };
 
@@ -601,12 +597,19 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // dz or g by column (global stores; out-of-image pixels go to the sink).  bf16: g is
   // rounded to bf16 first (as cnnitmo_bn_bwd_apply reads it from a bf16 buffer); fp32:
   // r of one column pair at a time (two 16-byte pieces per (pixel, 8 channels)).
-  auto epilogue_bnb16 = [&](const Pos& e, bool pre) {
+  auto epilogue_bnb16 = [&](const Pos& e) {
     const int oh0 = e.y0 + wave * RPW;
     const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
     const long m0 = ((long)e.img * p.ho + oh0) * p.wo + e.x0;  // the wave's first pixel
-    if (!pre) load_r16(e);
-    auto& rv = rvp;
+    dma::i32x4 rv[FM][FP];
+    {
+      const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int q = 0; q < FP; ++q) rv[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r_off(e, f, q), 0, 0);
+    }
+    load_route(e);
     // (also retires the next item's DMA, issued during this item's first taps).  Pulling
     // these pieces into L2 one item ahead by LDS-DMA into the sink measured 15-25 %
     // slower on every fused dgrad (dec6-dec8), whether issued before or after the
@@ -623,26 +626,24 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       lds8(par + cl, ca);
       lds8(par + BN + cl, cb);
       lds8(par + 2 * BN + cl, ce);
-      float ta[8], tb[8];  // SLOT: this tile's sums by pixel-row parity
-#pragma unroll
-      for (int k = 0; k < 8; ++k) ta[k] = tb[k] = 0.f;
-      float* sa_q = SLOT ? ta : sa[SLOT ? 0 : q];
-      float* sb_q = SLOT ? tb : sb[SLOT ? 0 : q];
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
         const bool ok = oh0 + rr < p.ho && e.x0 + col < p.wo;
         const long m = m0 + (long)rr * p.wo + col;
-        float v[8];
+        float v[8], gr[8];
+        routed(f, q, gr);
         const bf16x8 rq = __builtin_bit_cast(bf16x8, rv[f][q]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float gk = to_f32(from_f32<bf16>(acc[f][2 * q + (k >> 2)][k & 3]));
+          // (as cnnitmo_bn_bwd_apply_pooled: the bf16 gradient, then the routed pooled one)
+          float gk = to_f32(from_f32<bf16>(acc[f][2 * q + (k >> 2)][k & 3]));
+          if constexpr (POOL) gk += gr[k];
           const float r = to_f32(rq[k]);
           if (fz) {
             v[k] = to_f32(from_f32<bf16>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f));
-            sa_q[k] += (ok && rr == 0) ? v[k] : 0.f;
-            sb_q[k] += (ok && rr == 1) ? v[k] : 0.f;
+            sa[q][k] += (ok && rr == 0) ? v[k] : 0.f;
+            sb[q][k] += (ok && rr == 1) ? v[k] : 0.f;
           } else {
             v[k] = gk;
           }
@@ -651,30 +652,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
                      : fz ? reinterpret_cast<uint4*>(Z + (size_t)m * cbn + (c - c0))
                           : reinterpret_cast<uint4*>(O + (size_t)m * p.out_ld + p.out_off + c);
         *dst = __builtin_bit_cast(uint4, pack8(v));
-      }
-      if constexpr (SLOT) {
-        if (fz) {  // (uniform per 16-lane row: g)
-          // sum over the row's lanes of equal pixel-column parity: rotate-adds by 2, 4, 8
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            ta[k] += dpp_ror<2>(ta[k]);
-            tb[k] += dpp_ror<2>(tb[k]);
-            ta[k] += dpp_ror<4>(ta[k]);
-            tb[k] += dpp_ror<4>(tb[k]);
-            ta[k] += dpp_ror<8>(ta[k]);
-            tb[k] += dpp_ror<8>(tb[k]);
-          }
-          if (pxl < 2) {  // slot [wave][row parity * 2 + column parity][BN]
-            float* sl = utb + (wave * 4 + pxl) * BN + cl;
-            float4* s0 = reinterpret_cast<float4*>(sl);
-            float4* s1 = reinterpret_cast<float4*>(sl + 2 * BN);
-            const float4 a0 = s0[0], a1 = s0[1], b0 = s1[0], b1 = s1[1];
-            s0[0] = float4{a0.x + ta[0], a0.y + ta[1], a0.z + ta[2], a0.w + ta[3]};
-            s0[1] = float4{a1.x + ta[4], a1.y + ta[5], a1.z + ta[6], a1.w + ta[7]};
-            s1[0] = float4{b0.x + tb[0], b0.y + tb[1], b0.z + tb[2], b0.w + tb[3]};
-            s1[1] = float4{b1.x + tb[4], b1.y + tb[5], b1.z + tb[6], b1.w + tb[7]};
-          }
-        }
       }
     }
     zero_acc();
@@ -706,6 +683,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     };
     TE* __restrict__ O = (TE*)p.out;
     TE* __restrict__ Z = (TE*)p.bnb_out;
+    load_route(e);  // (retired by load_r's wait)
     if constexpr (ES == 2) load_r(0);
 #pragma unroll
     for (int q = 0; q < FP; ++q) {
@@ -722,7 +700,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
         const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
         const bool ok = oh0 + rr < p.ho && e.x0 + col < p.wo;
         const long m = m0 + (long)rr * p.wo + col;
-        float v[8], rf[8];
+        float v[8], rf[8], gr[8];
+        routed(f, q, gr);
         if constexpr (ES == 2) {
           const bf16x8 rq = __builtin_bit_cast(bf16x8, rv[f][qr][0]);
 #pragma unroll
@@ -737,7 +716,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float gk = to_f32(from_f32<TE>(acc[f][2 * q + (k >> 2)][k & 3]));
+          float gk = to_f32(from_f32<TE>(acc[f][2 * q + (k >> 2)][k & 3]));
+          if constexpr (POOL) gk += gr[k];
           const float r = rf[k];
           if (fz) {
             v[k] = to_f32(from_f32<TE>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f));
@@ -762,8 +742,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     zero_acc();
   };
 
-  auto epilogue_bnb = [&](const Pos& e, bool pre) {
-    if constexpr (ES == 2) epilogue_bnb16(e, pre);
+  auto epilogue_bnb = [&](const Pos& e) {
+    if constexpr (ES == 2) epilogue_bnb16(e);
     else epilogue_bnb32(e);
   };
 
@@ -805,15 +785,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const bool pf = t + ST - 1 < T;
     if (pf) issue_prep(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
     const bool act = ep.y0 + wave * RPW < p.ho;
-    const bool rl = HALO_RTAP && EPI == 2 && ES == 2 && act && ep.ch == nch - 1;
-    if constexpr (HALO_RTAP && EPI == 2 && ES == 2) {  // no value carried between items
-#pragma unroll
-      for (int f = 0; f < FM; ++f)
-#pragma unroll
-        for (int q = 0; q < FP; ++q) rvp[f][q] = __builtin_nondeterministic_value(rvp[f][q]);
-    }
     if (act) {
-      compute(buf, pf, ep.ch, rl ? &ep : nullptr);  // issues those loads between its taps
+      compute(buf, pf, ep.ch);  // issues those loads between its taps
     } else if (pf) {     // the wave's rows are all below the frame: no MFMAs, DMA share only
 #pragma unroll
       for (int q = 0; q < L; ++q) issue_piece(q);
@@ -824,7 +797,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       mq[ST - 1] = issued;
     }
     if (ep.ch == nch - 1) {
-      if constexpr (EPI == 2) epilogue_bnb(ep, rl);
+      if constexpr (EPI == 2) epilogue_bnb(ep);
       else epilogue(ep);
       issued += NST;
     }
@@ -856,31 +829,6 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
             st[32 * q + 8 * g + k] = sa[q][k];
             st[p.N + 32 * q + 8 * g + k] = sb[q][k];
           }
-      }
-    }
-  } else if constexpr (SLOT) {
-    const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
-    if (pxl < 2) {
-      const int cp = pxl;  // pixel-column parity
-      const float* sl = utb + wave * 4 * BN;
-#pragma unroll
-      for (int q = 0; q < FP; ++q) {
-        const int cl = 32 * q + 8 * g, c = n0 + cl;
-        if (c >= c0 && c < c1) {
-          if (p.bnb_par) {
-            float* st = p.stats + (size_t)row * 4 * cbn + (c - c0);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              st[(size_t)(0 * 2 + cp) * cbn + k] = sl[(0 * 2 + cp) * BN + cl + k];
-              st[(size_t)(1 * 2 + cp) * cbn + k] = sl[(1 * 2 + cp) * BN + cl + k];
-            }
-          } else if (cp == 0) {
-            float* st = p.stats + (size_t)row * cbn + (c - c0);
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              st[k] = (sl[cl + k] + sl[2 * BN + cl + k]) + (sl[BN + cl + k] + sl[3 * BN + cl + k]);
-          }
-        }
       }
     }
   } else if constexpr (EPI == 2) {
@@ -968,8 +916,10 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   if (a.a2 && (a.cin1 % 32 || a.cin1 <= 0 || a.cin1 >= a.cin || a.a2_ld % 8 || a.a2_off % 8 || a.bnb_out))
     return false;
   if (a.ntaps != 9 || a.scale != 1 || a.scatter || a.hs != a.ho || a.ws != a.wo) return false;
-  if (a.pool_out && (a.a2 || a.bnb_out || a.ho % 2 || a.wo % 2 || a.pool_ld % 8 || a.pool_ld < a.N || !a.pool_idx))
+  if (a.pool_out && (a.a2 || a.ho % 2 || a.wo % 2 || a.pool_ld % 8 || a.pool_ld < a.N || !a.pool_idx))
     return false;
+  // the routed pooled gradient (EPI 2): every column BN-fused, pooled [..][N] rows
+  if (a.pool_out && a.bnb_out && (a.bnb_c0 != 0 || a.bnb_c1 != a.N || a.pool_ld != a.N || a.bnb_par)) return false;
   // pooled forward: BN sums (training, BN folded: r stored) or the affine (inference), not both
   if (a.pool_out && (a.flags & CNNITMO_STATS) && (a.flags & CNNITMO_AFFINE)) return false;
   pl.bn = a.N % 64 == 0 ? 64 : (a.N % 32 == 0 ? 32 : 0);
@@ -993,29 +943,16 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
     return e ? atoi(e) : 1;
   }();
   pl.res = res && a.cin <= (f32 ? 16 : 32) * RCH;
-  // dec9a's forward (cin 96 = the [conv1 32 | up9 64] concat, 64 output channels, one column
-  // block): 8-row tiles with all three weight chunks resident (2 x 22 KB patches + 108 KB
-  // weights) instead of 16-row tiles streaming 36 KB of weights per 32-channel item.
-  // Off by default (CNNITMO_HALO_TH8=1 enables it): 8.00 vs 7.85 ms on dec9a's forward
-  // (profiles/r04b_th8_ab.txt; twice the halo rows per output row, and half the MFMAs
-  // per barrier)
-  static const int th8 = [] {
-    const char* e = getenv("CNNITMO_HALO_TH8");
-    return e ? atoi(e) : 0;
-  }();
   pl.th = 16;
-  if (th8 && !f32 && pl.epi == 1 && pl.bn == 64 && a.N == 64 && a.cin == 96 && !a.pool_out && res) {
-    pl.th = 8;
-    pl.res = true;
-  }
   return true;
 }
 
 template <typename T, int BN, int EPI>
-void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s, int th = 16) {
-  if constexpr (EPI == 1 && BN == 64 && sizeof(T) == 2) {
-    if (th == 8) {  // (halo_plan: resident weights, no pooling)
-      hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, false, 8>), dim3(grid), dim3(NT), 0, s, h);
+void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
+  if constexpr (EPI == 2) {
+    if (h.f.pool_out) {  // the routed pooled gradient (cnnitmo_conv3x3_dgrad_bn_pooled)
+      if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
+      else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true>), dim3(grid), dim3(NT), 0, s, h);
       return;
     }
   }
@@ -1082,7 +1019,7 @@ int launch_halo(FwdArgs a, hipStream_t s, const char* what, bool f32) {
   } else if (pl.epi == 3) {
     launch_cfg<bf16, 64, 3>(h, pl.res, grid, s);
   } else if (pl.epi == 1) {
-    if (pl.bn == 64) launch_cfg<bf16, 64, 1>(h, pl.res, grid, s, pl.th);
+    if (pl.bn == 64) launch_cfg<bf16, 64, 1>(h, pl.res, grid, s);
     else launch_cfg<bf16, 32, 1>(h, pl.res, grid, s);
   } else {
     if (pl.bn == 64) launch_cfg<bf16, 64, 0>(h, pl.res, grid, s);
@@ -1096,7 +1033,7 @@ const char* halo_name(const FwdArgs& a, bool f32) {
   if (!halo_plan(a, pl, f32)) return "";
   static thread_local char buf[64];
   snprintf(buf, sizeof(buf), "halo_conv_kernel<%s%d,%d%s%s>", f32 ? "f32," : "", pl.bn, pl.epi, pl.res ? ",wres" : "",
-           pl.th == 8 ? ",th8" : "");
+           a.pool_out ? (pl.epi == 2 ? ",route" : ",pool") : "");
   return buf;
 }
 

@@ -9,6 +9,7 @@
 namespace dma {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // voffset at or beyond num_records: a load lands zeros, a store is dropped
 constexpr unsigned OOB = 0x80000000u;

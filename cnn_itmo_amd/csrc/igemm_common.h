@@ -155,13 +155,6 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
                     const float* aff_scale, const float* aff_shift, float* stats, hipStream_t s, const char* what,
                     bool f32 = false);
 
-// tconv_kc.hip: bf16 Conv2DTranspose input gradient at K = 4*cout = 1024 / 2048 (up6, up7),
-// weights streamed through LDS in K chunks, A straight into registers
-bool tconv_kc_handles(int cin, int cout);
-const char* tconv_kc_name(int cin, int cout);
-int launch_tconv_kc(const void* dout, int n, int h, int w, int cout, const void* kT, int cin, void* dx, hipStream_t s,
-                    const char* what);
-
 // v2 (direct-to-LDS, multi-tap) bf16 weight gradients, igemm_wgrad2.hip
 struct Wgrad2Args {
   const bf16* a;  // A operand source (gradient): channels m

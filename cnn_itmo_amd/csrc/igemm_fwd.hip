@@ -525,7 +525,6 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
     return tconv_ws_name(dgrad ? 1 : 0, cin, cout);
   if (dtype == CNNITMO_F32 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout, true))
     return tconv_ws_name(dgrad ? 1 : 0, cin, cout, true);
-  if (dtype == CNNITMO_BF16 && dgrad && tconv_kc_handles(cin, cout)) return tconv_kc_name(cin, cout);
   FwdArgs a = base_args();
   a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
   a.cin = dgrad ? cout : cin;
@@ -625,6 +624,48 @@ extern "C" int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h,
   return launch_halo(a, (hipStream_t)stream, "conv3x3_dgrad_bn", f32);
 }
 
+namespace {
+FwdArgs dgrad_bn_pooled_args(int n, int h, int w, int cout, int cin) {
+  FwdArgs a = dgrad_bn_args(n, h, w, cout, cin);
+  a.bnb_c0 = 0; a.bnb_c1 = cin; a.bnb_out = (void*)1; a.bnb_r_ld = cin;
+  a.pool_out = (void*)1; a.pool_ld = cin; a.pool_idx = (unsigned char*)1;
+  return a;
+}
+}  // namespace
+
+// Partial-sum rows cnnitmo_conv3x3_dgrad_bn_pooled writes (0: not available for these sizes).
+extern "C" long cnnitmo_conv3x3_dgrad_bn_pooled_rows(int dtype, int n, int h, int w, int cout, int cin) {
+  FwdArgs a = dgrad_bn_pooled_args(n, h, w, cout, cin);
+  const bool f32 = dtype == CNNITMO_F32;
+  if ((dtype != CNNITMO_BF16 && !f32) || !halo_handles(a, f32)) return 0;
+  return halo_stat_rows(a, f32);
+}
+
+extern "C" const char* cnnitmo_conv3x3_dgrad_bn_pooled_kernel_name(int dtype, int n, int h, int w, int cout,
+                                                                   int cin) {
+  FwdArgs a = dgrad_bn_pooled_args(n, h, w, cout, cin);
+  const bool f32 = dtype == CNNITMO_F32;
+  if ((dtype != CNNITMO_BF16 && !f32) || !halo_handles(a, f32)) return "";
+  return halo_name(a, f32);
+}
+
+extern "C" int cnnitmo_conv3x3_dgrad_bn_pooled(int dtype, const void* dz, int n, int h, int w, int cout,
+                                               const void* wt_flip, int cin, const float* coef, const void* r,
+                                               int r_ld, int r_off, const void* dy_pool, const unsigned char* idx,
+                                               void* dz_out, float* part, void* stream) {
+  FwdArgs a = dgrad_bn_pooled_args(n, h, w, cout, cin);
+  a.a = dz; a.b = wt_flip;
+  a.out = dz_out; a.out_ld = cin; a.out_off = 0;
+  a.bnb_coef = coef; a.bnb_r = r; a.bnb_r_ld = r_ld; a.bnb_r_off = r_off; a.bnb_out = dz_out;
+  a.pool_out = const_cast<void*>(dy_pool); a.pool_idx = const_cast<unsigned char*>(idx);
+  a.stats = part;
+  const bool f32 = dtype == CNNITMO_F32;
+  CNN_REQUIRE((dtype == CNNITMO_BF16 || f32) && halo_handles(a, f32),
+              "conv3x3_dgrad_bn_pooled: unsupported sizes (halo kernel, even h and w)");
+  CNN_REQUIRE(coef && r && dy_pool && idx && dz_out && part, "conv3x3_dgrad_bn_pooled: missing buffers");
+  return launch_halo(a, (hipStream_t)stream, "conv3x3_dgrad_bn_pooled", f32);
+}
+
 extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int w, int cin,
                                     const void* k, const float* bias, int cout, void* out,
                                     int out_ld, int out_off, int flags, const float* aff_scale,
@@ -668,8 +709,6 @@ extern "C" int cnnitmo_tconv2x2_dgrad(int dtype, const void* dout, int n, int h,
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(1, cin, cout))
     return launch_tconv_ws(1, dout, cout, 0, kT, n, h, w, cin, cout, dx, cin, 0, nullptr, 0, nullptr, nullptr,
                            nullptr, (hipStream_t)stream, "tconv2x2_dgrad");
-  if (dtype == CNNITMO_BF16 && tconv_kc_handles(cin, cout))
-    return launch_tconv_kc(dout, n, h, w, cout, kT, cin, dx, (hipStream_t)stream, "tconv2x2_dgrad");
   if (dtype == CNNITMO_F32 && tconv_ws_handles(1, cin, cout, true))
     return launch_tconv_ws(1, dout, cout, 0, kT, n, h, w, cin, cout, dx, cin, 0, nullptr, 0, nullptr, nullptr,
                            nullptr, (hipStream_t)stream, "tconv2x2_dgrad", true);

@@ -65,6 +65,9 @@ class Value:
         self.bn_contrib = []  # per-step partial-sum tensors [rows][2][c] from the consumers
         self.pool_route = None  # (pooled gradient, argmax idx): a deferred MaxPooling2D backward
         self.grad_g3 = None  # (g3 [p][3], head weights [3][c]): the gradient as the head's rank-3 factor
+        # a deferred skip-path input gradient (dz, n, h, w, cout, flipped weights, c) of the concat
+        # consumer: computed inside this value's BN backward (cnnitmo_conv3x3_dgrad_bn_pooled)
+        self.gdefer = None
         self.cs = None  # coefficient buffers of the owner (persist across steps)
         self.ch = None
         self.split = False  # concat whose members keep dense buffers of their own (Engine._plan_split_concats)
@@ -133,6 +136,7 @@ class Value:
         self.bn_contrib = []
         self.pool_route = None
         self.grad_g3 = None
+        self.gdefer = None
 
 
 class Stage:
@@ -381,7 +385,7 @@ class BlockStage(Stage):
         if not self.vout.ginit:
             raise RuntimeError(f"{self.name}: output gradient not initialised")
         g3 = self.vout.grad_g3
-        dy = self.vout.gview(n) if g3 is None else None
+        dy = self.vout.gview(n) if g3 is None and self.vout.gdefer is None else None
         rows = ops.bn_bwd_rows(P, cout)
         dz = torch.empty(P * cout, dtype=e.tdtype, device=e.device)
         part2 = torch.empty(rows * (4 if par else 1) * cout, device=e.device, dtype=torch.float32)
@@ -410,6 +414,17 @@ class BlockStage(Stage):
                 assert not flags and v.pool_route is None, "rank-3 head gradient with dropout/parity/pool"
                 ops.bn_bwd_apply_g3(e.dt, g3[0], g3[1], self.r, cout, P, coef, dz, part2)
                 v.grad_g3 = None
+            elif v.pool_route is not None and v.gdefer is not None:
+                # the concat consumer's skip-path dgrad, deferred to here: its gradient is never
+                # stored, the pool's is routed in, the BN backward applied (one launch)
+                assert not flags, "pool routing with dropout/parity"
+                dzs, hs, ws, cz, wb = v.gdefer
+                rows = ops.conv3x3_dgrad_bn_pooled_rows(e.dt, n, hs, ws, cz, cout)
+                part2 = torch.empty(rows * cout, device=e.device, dtype=torch.float32)
+                ops.conv3x3_dgrad_bn_pooled(e.dt, dzs, n, hs, ws, cz, wb, cout, coef, self.r, v.pool_route[0],
+                                            v.pool_route[1], dz, part2)
+                v.pool_route = None
+                v.gdefer = None
             elif v.pool_route is not None:
                 assert not flags, "pool routing with dropout/parity"
                 ops.bn_bwd_apply_pooled(e.dt, dy, self.r, cout, coef, v.pool_route[0], v.pool_route[1], dz,
@@ -454,6 +469,24 @@ class BlockStage(Stage):
         if len(ms) == 1 and ms[0].place[1] == 0 and ms[0].c == ci0 and not ms[0].ginit:
             return ms[0]
         return None
+
+    def _defer_skip(self, skip, n):
+        """dec9's skip path (conv1, model.py:209-211 + 261): when conv1's only other reader is
+        pool1 and its BN-backward sums come from its consumers, its input gradient is not
+        launched here but inside conv1's BN backward, where pool1's gradient is routed in
+        (cnnitmo_conv3x3_dgrad_bn_pooled): the 32-channel skip gradient is neither written
+        nor read back, and the stand-alone pooled BN-backward apply disappears.
+        CNNITMO_DEFER_SKIP=0: the separate dgrad + bn_bwd_apply_pooled."""
+        e = self.eng
+        if os.environ.get("CNNITMO_DEFER_SKIP", "1") == "0" or not e.fuse_bnb:
+            return False
+        prod = skip.producer
+        if prod is None or prod.bn is None or prod.drop is not None or not skip.folded or skip.sum_consumers != 2:
+            return False
+        pools = [s for s in e.stages if isinstance(s, PoolStage) and s.vin is skip]
+        if len(pools) != 1 or prod.kind == "t2":
+            return False
+        return ops.conv3x3_dgrad_bn_pooled_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, skip.c) > 0
 
     def _split_fused(self, ci0, c):
         """dec9's input gradient (concat [skip 32 | up 64], model.py:261): two launches
@@ -541,13 +574,18 @@ class BlockStage(Stage):
             pp = torch.empty(frows * (4 if ppar else 1) * m.c, device=e.device, dtype=torch.float32)
             if split:
                 h, w = self.vout.h, self.vout.w
-                if skip is not None:  # dense skip gradient: full-line traffic for the pool / BN backward
-                    skip.gsep = True
-                    skip.ensure_grad(n, e.tdtype, e.device)
-                    dxs = skip.gview(n)
+                if skip is not None and self._defer_skip(skip, n):
+                    # the skip member's gradient is computed later, inside its producer's BN
+                    # backward, together with its pool's routed gradient (_bn_backward)
+                    skip.gdefer = (dz, h, w, cout, self.w_bwd)
                 else:
-                    dxs = ops.View(dx.buf, n, h, w, ci0, dx.ld, dx.off)
-                ops.conv3x3_dgrad(e.dt, dz, n, h, w, cout, self.w_bwd, ci0, dxs)
+                    if skip is not None:  # dense skip gradient: full-line traffic for the pool / BN backward
+                        skip.gsep = True
+                        skip.ensure_grad(n, e.tdtype, e.device)
+                        dxs = skip.gview(n)
+                    else:
+                        dxs = ops.View(dx.buf, n, h, w, ci0, dx.ld, dx.off)
+                    ops.conv3x3_dgrad(e.dt, dz, n, h, w, cout, self.w_bwd, ci0, dxs)
                 wsub = self.w_bwd[ci0 * 9 * cout:]  # flipped weights [cin][3][3][cout]: rows ci0..
                 ops.conv3x3_dgrad_bn(e.dt, dz, n, h, w, cout, wsub, m.c, None, 0, m.c, coef, prod.r, dzp, pp, ppar)
             elif self.kind == "c3":

@@ -136,6 +136,18 @@ def conv3x3_dgrad_bn(dt, dz, n, h, w, cout, wflip, cin, dx, c0, c1, coef, r, dz_
          c0, c1, ptr(coef), rp, rld, roff, ptr(dz_out), ptr(part), 1 if parity else 0, stream_ptr())
 
 
+def conv3x3_dgrad_bn_pooled_rows(dt, n, h, w, cout, cin):
+    return query("cnnitmo_conv3x3_dgrad_bn_pooled_rows", dt, n, h, w, cout, cin)
+
+
+def conv3x3_dgrad_bn_pooled(dt, dz, n, h, w, cout, wflip, cin, coef, r, dyp, idx, dz_out, part):
+    """The skip member's input gradient + its MaxPooling2D gradient routed by idx, through the
+    producer's BN backward (cnnitmo_conv3x3_dgrad_bn_pooled): the skip gradient is never stored."""
+    rp, rld, roff = _rview(r, cin)
+    call("cnnitmo_conv3x3_dgrad_bn_pooled", dt, ptr(dz), n, h, w, cout, ptr(wflip), cin, ptr(coef), rp, rld, roff,
+         ptr(dyp), ptr(idx), ptr(dz_out), ptr(part), stream_ptr())
+
+
 def tconv_dgrad_bn_rows(dt, n, h, w, cout, cin):
     return query("cnnitmo_tconv2x2_dgrad_bn_rows", dt, n, h, w, cout, cin)
 

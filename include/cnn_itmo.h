@@ -158,6 +158,22 @@ int cnnitmo_conv3x3_dgrad_bn(int dtype, const void* dz, int n, int h, int w, int
 /* Label of the kernel cnnitmo_conv3x3_dgrad_bn launches ("" = unavailable; profiling only). */
 const char* cnnitmo_conv3x3_dgrad_bn_kernel_name(int dtype, int n, int h, int w, int cout, int cin,
                                                  int c0, int c1);
+/* The skip path of a concatenate whose other reader is a MaxPooling2D(2) (model.py:209-211
+ * + 261: conv1 feeds pool1 and merge9): the input-gradient of the concat-consuming conv
+ * for the skip member's cin channels (wt_flip: its rows [cin][3][3][cout] of the flipped
+ * weights), PLUS the pool's gradient dy_pool [n,h/2,w/2,cin] (dense) routed to the window
+ * position idx [n,h/2,w/2,cin] (bytes, first-max index in window order, as
+ * cnnitmo_maxpool2x2_fwd / _fwd_pool write them), through the producer's BN backward:
+ * dz_out [n*h*w][cin] = [r>0]*(a*(bf16(g) + routed) - b*r + e), column-sum partials part
+ * [rows][cin] (rows = cnnitmo_conv3x3_dgrad_bn_pooled_rows; 0: unavailable).  h, w even.
+ * Replaces conv3x3_dgrad + cnnitmo_bn_bwd_apply_pooled (the skip gradient is never
+ * stored). */
+long cnnitmo_conv3x3_dgrad_bn_pooled_rows(int dtype, int n, int h, int w, int cout, int cin);
+int cnnitmo_conv3x3_dgrad_bn_pooled(int dtype, const void* dz, int n, int h, int w, int cout,
+                                    const void* wt_flip, int cin, const float* coef, const void* r, int r_ld,
+                                    int r_off, const void* dy_pool, const unsigned char* idx, void* dz_out,
+                                    float* part, void* stream);
+const char* cnnitmo_conv3x3_dgrad_bn_pooled_kernel_name(int dtype, int n, int h, int w, int cout, int cin);
 
 /* Weight-gradient of conv3x3 (TF Conv2DBackpropFilter).  x view [n,h,w,cin];
  * dz [n,h,w,cout] contiguous; dw: [cout][3][3][cin] fp32, OVERWRITTEN.

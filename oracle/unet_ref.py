@@ -431,15 +431,24 @@ class UNetRef:
         grads[name + "/bias"] = db
         return None if dx is None else self.q(dx)
 
-    def backward(self, target):
-        """MSE loss on the last forward; returns (loss, acc, grads)."""
+    def backward(self, target, valid_rows=None):
+        """MSE loss on the last forward; returns (loss, acc, grads).  valid_rows: the loss and
+        metric cover only output rows < valid_rows (U_net(pad=True)'s zero-padded frames:
+        target [n, valid_rows, w, 3], padded rows get no loss gradient)."""
         c = self.cache
         t = np.asarray(target, self.dtype)
         yhat = c["yhat"]
-        loss = mse(yhat, t)
-        acc = categorical_accuracy(t, yhat)
+        if valid_rows is not None:
+            yv = yhat[:, :valid_rows]
+            loss = mse(yv, t)
+            acc = categorical_accuracy(t, yv)
+            dz = np.zeros_like(yhat)
+            dz[:, :valid_rows] = mse_grad_z(yv, t)
+        else:
+            loss = mse(yhat, t)
+            acc = categorical_accuracy(t, yhat)
+            dz = mse_grad_z(yhat, t)
         grads = {}
-        dz = mse_grad_z(yhat, t)
         dx9, dw, db = conv2d_same_bwd(c["head_x"], self.P["conv2d_15/kernel"], dz)
         grads["conv2d_15/kernel"] = dw
         grads["conv2d_15/bias"] = db

@@ -126,8 +126,8 @@ class _Acc:
 
 
 # every launching entry point of cnn_itmo_amd.ops (all of them go through ops.call)
-LAUNCHES = ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_head", "pool_bnsums_pooled", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "tconv_fwd", "tconv_dgrad", "tconv_dgrad_bn",
-            "conv_wgrad", "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad", "conv1tap_fwd", "im2col_c3",
+LAUNCHES = ("conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_head", "pool_bnsums_pooled", "conv3x3_fwd_cat", "conv_wgrad_cat", "conv3x3_dgrad", "conv3x3_dgrad_bn", "conv3x3_dgrad_bn_pooled", "tconv_fwd", "tconv_dgrad",
+            "tconv_dgrad_bn", "conv_wgrad", "tconv_wgrad", "conv_c3_fwd", "conv_c3_wgrad", "conv1tap_fwd", "im2col_c3",
             "maxpool_fwd", "maxpool_bwd", "pool_bnsums", "bn_fwd_finalize", "bn_infer_coeffs", "bn_apply",
             "bn_bwd_reduce", "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3",
             "bn_consumer_sums", "colsum", "border_sums", "head_fwd", "head_fwd_bwd", "head_fwd_bwd_g3",
@@ -322,6 +322,33 @@ class LaunchChecker(ElementwiseChecks):
             accx.done()
         tot = part.view(-1, npar, c).to(F64).sum(0)
         self._sums(lab + " part", tot, ps, pa)
+
+    def _chk_conv3x3_dgrad_bn_pooled(self, dt, dz, n, h, w, cout, wflip, cin, coef, r, dyp, idx, dz_out, part):
+        """dz = [r>0]*(a*(bf16(g) + routed) - b*r + e): g the exact skip-path input gradient,
+        routed = the pooled gradient at the window position its index byte names."""
+        lab = f"conv3x3_dgrad_bn_pooled {n}x{h}x{w} {cout}->{cin}"
+        d4, Wf = dz.view(n, h, w, cout), wflip.view(-1)[:cin * 9 * cout].view(cin, 3, 3, cout)
+        rt, zo = self._rtensor(r, n, h, w, cin), dz_out.view(n, h, w, cin)
+        gp, ix = dyp.view(n, h // 2, w // 2, cin), idx.view(n, h // 2, w // 2, cin)
+        a, b, e = coef.view(3, cin).to(F64)
+        acc = _Acc(self, lab)
+        ps = torch.zeros(1, cin, dtype=F64, device=dz.device)
+        pa = torch.zeros_like(ps)
+        for i in range(n):
+            g = _conv3(d4[i], Wf)
+            routed = torch.zeros_like(g)
+            gpi, ixi = gp[i].to(F64), ix[i]
+            for k in range(4):
+                routed[k // 2::2, k % 2::2] = torch.where(ixi == k, gpi, torch.zeros_like(gpi))
+            gb = (g.to(BF).to(F64) if self.dt == L.BF16 else g) + routed
+            rd = rt[i].to(F64)
+            ref = torch.where(rd > 0, a * gb - b * rd + e, torch.zeros_like(gb))
+            extra = 2.0 ** -7 * (a * g).abs() if self.dt == L.BF16 else None
+            acc.add(zo[i], ref, extra)
+            ps[0] += zo[i].to(F64).sum((0, 1))
+            pa[0] += zo[i].to(F64).abs().sum((0, 1))
+        acc.done()
+        self._sums(lab + " part", part.view(-1, 1, cin).to(F64).sum(0), ps, pa)
 
     def _chk_conv_wgrad(self, dt, ntaps, x, dz, cout, dw, dw_cols=0, fold=None, raw=None, tag=""):
         n, h, w, cin = x.n, x.h, x.w, x.c

@@ -311,6 +311,62 @@ def test_conv3x3_dgrad_bn_fused(cin, cout, H, W, c0, c1, par, dt):
         assert float(np.abs(gx[:, c0:c1]).max()) == 0.0  # fused columns are not written to dx
 
 
+@pytest.mark.parametrize("cin,cout,H,W", [
+    (32, 64, 20, 40),     # dec9's skip path (conv1 32 of the [32 | 64] concat), partial tiles
+    (32, 64, 34, 70),     # ragged in both directions (partial 16-row tiles, 32-column strips)
+    (64, 128, 16, 32),    # BN 64 (a level-1 skip path)
+    (32, 96, 18, 66)])
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+def test_conv3x3_dgrad_bn_pooled(cin, cout, H, W, dt):
+    """cnnitmo_conv3x3_dgrad_bn_pooled == conv3x3_dgrad of the skip rows, then
+    bn_bwd_apply_pooled (the pooled gradient routed by the window index bytes) with
+    the same coefficients: the deferred skip gradient of dec9 fused with conv1's
+    MaxPooling2D route and BN backward."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin + cout + H + W)
+    N, d = 2, DT[dt]
+    T = TDT[dt]
+    cl = cin + 64  # the concat consumer's input channels: skip rows [0, cin) of its flipped weights
+    w = (rng.standard_normal((cout, 3, 3, cl)) * 0.1).astype(np.float32)
+    wf = torch.empty(w.size, dtype=T, device="cuda")
+    wflip = torch.empty(w.size, dtype=T, device="cuda")
+    ops.prep_conv3x3(d, torch.tensor(w).cuda(), cout, cl, wf, wflip)
+    dz = dev(rng.standard_normal((N, H, W, cout)).astype(np.float32), dt).reshape(-1)
+    rb = dev(np.maximum(rng.standard_normal((N, H, W, cin)), 0).astype(np.float32), dt).reshape(-1)
+    rv = ops.View(rb, N, H, W, cin, cin, 0)
+    dyp = dev(rng.standard_normal((N, H // 2, W // 2, cin)).astype(np.float32), dt).reshape(-1)
+    idx = torch.tensor(rng.integers(0, 4, (N, H // 2, W // 2, cin)).astype(np.uint8).reshape(-1)).cuda()
+    coef = cu(rng.standard_normal(3 * cin).astype(np.float32))
+    P = N * H * W
+    # unfused reference path: the skip gradient stored, then the pooled BN-backward apply
+    g = torch.zeros(P * cin, dtype=T, device="cuda")
+    gv = ops.View(g, N, H, W, cin, cin, 0)
+    ops.conv3x3_dgrad(d, dz, N, H, W, cout, wflip, cin, gv)
+    rows = ops.bn_bwd_rows(P, cin)
+    pref = torch.empty(rows * cin, device="cuda")
+    zref = torch.empty(P * cin, dtype=T, device="cuda")
+    ops.bn_bwd_apply_pooled(d, gv, rv, cin, coef, dyp, idx, zref, pref)
+    sref = torch.empty(cin, device="cuda")
+    ops.colsum(pref, rows, cin, 1, sref)
+    # fused
+    frows = ops.conv3x3_dgrad_bn_pooled_rows(d, N, H, W, cout, cin)
+    assert frows > 0
+    zf = torch.full((P * cin,), float("nan"), dtype=T, device="cuda")
+    pf = torch.empty(frows * cin, device="cuda")
+    ops.conv3x3_dgrad_bn_pooled(d, dz, N, H, W, cout, wflip, cin, coef, rv, dyp, idx, zf, pf)
+    sf = torch.empty(cin, device="cuda")
+    ops.colsum(pf, frows, cin, 1, sf)
+    torch.cuda.synchronize()
+    a, b = host(zf), host(zref)
+    assert np.isfinite(a).all()
+    if dt == "f32":  # the same fp32 g and formula (up to an fma contraction)
+        assert np.abs(a - b).max() <= 1e-5 * max(1.0, np.abs(b).max())
+    else:  # the same bf16-rounded g; an fp32 contraction difference may flip one bf16 rounding
+        assert np.abs(a - b).max() <= 1e-2 * max(1.0, np.abs(b).max())
+        assert np.mean(a != b) < 1e-3
+    np.testing.assert_allclose(host(sf), host(sref), rtol=1e-4, atol=1e-2)
+
+
 @pytest.mark.parametrize("cin,cout,H,W", [(128, 64, 3, 70), (64, 32, 4, 64), (128, 32, 2, 130)])
 def test_tconv_dgrad_bn_fused(cin, cout, H, W):
     """cnnitmo_tconv2x2_dgrad_bn == tconv2x2_dgrad followed by bn_bwd_apply (r from a view)."""

@@ -143,8 +143,8 @@ def test_conv_affine_inference_epilogue(dt, H, W):
                                           # bf16 weight-stationary kernel: fwd at 32 column blocks
                                           # (512 -> 512), dgrad at BN 128 (256 <- 128); ragged tiles
                                           (512, 512, 3, 7), (256, 128, 7, 9),
-                                          # 1024 / 2048-deep gradients (up7 / up6: tconv_kc, weight
-                                          # chunks through LDS; ragged 256-pixel passes, 2 or 4 blocks)
+                                          # 1024 / 2048-deep gradients (up7 / up6: igemm_fwd2's
+                                          # 256 x 256 tiles; ragged tiles)
                                           (512, 256, 5, 7), (512, 256, 17, 33), (256, 512, 9, 31),
                                           # bf16 row-streaming wgrad: 4 rows per workgroup, 2 strips
                                           (512, 512, 16, 40)])
@@ -457,6 +457,23 @@ def test_conv3x3_fwd_pool(dt, cin, cout, H, W):
         first = (key == key.max(3, keepdim=True).values).to(torch.uint8).argmax(3)
         assert torch.equal(pi.view(N, H // 2, W // 2, cout), first.to(torch.uint8))
         assert torch.equal(pv.view(N, H // 2, W // 2, cout), y.gather(3, first.unsqueeze(3)).squeeze(3))
+    # the inference kernel predict() launches: ReLU + the BN affine (negative scales too) applied
+    # before pooling, no sums (the NOSUM instantiation); pooled by the maximum of the stored y
+    sc = torch.tensor(np.resize([1.5, -0.75, 0.25, -2.0], cout).astype(np.float32)).cuda()
+    sh = torch.tensor(rng.standard_normal(cout).astype(np.float32)).cuda()
+    refa = ops.new_view(N, H, W, cout, T)
+    ops.conv3x3_fwd(d, xv, wf, bias, refa, 1 | 4, aff=(sc, sh))
+    out = ops.new_view(N, H, W, cout, T)
+    pv = torch.empty(N * (H // 2) * (W // 2) * cout, dtype=T, device="cuda")
+    pi = torch.empty(N * (H // 2) * (W // 2) * cout, dtype=torch.uint8, device="cuda")
+    ops.conv3x3_fwd_pool(d, xv, wf, bias, out, pv, pi, None, flags=1 | 4, aff=(sc, sh))
+    torch.cuda.synchronize()
+    assert torch.equal(out.buf, refa.buf)
+    y = refa.buf.view(N, H // 2, 2, W // 2, 2, cout).permute(0, 1, 3, 2, 4, 5).reshape(N, H // 2, W // 2, 4, cout)
+    key = y.double()
+    first = (key == key.max(3, keepdim=True).values).to(torch.uint8).argmax(3)
+    assert torch.equal(pi.view(N, H // 2, W // 2, cout), first.to(torch.uint8))
+    assert torch.equal(pv.view(N, H // 2, W // 2, cout), y.gather(3, first.unsqueeze(3)).squeeze(3))
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f32"])
@@ -494,45 +511,30 @@ def test_conv3x3_fwd_head(dt, cin, H, W, hv):
 
 
 @pytest.mark.parametrize("H,W", [(16, 64), (20, 70), (8, 40)])
-@pytest.mark.parametrize("th8", ["1", "0"])
-def test_conv3x3_fwd_cat_dec9a(H, W, th8):
-    """cnnitmo_conv3x3_fwd_cat on dec9a's shape ([conv1 32 | up9 64] -> 64, model.py:261-262)
-    vs the oracle on the materialised concat: ReLU + BN sums, with the 8-row resident-weight
-    tiles (default) and with the 16-row streamed ones (CNNITMO_HALO_TH8=0, read once per
-    process: run in a subprocess)."""
-    import subprocess
-    import sys as _sys
-    code = f"""
-import sys, numpy as np, torch
-sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
-from cnn_itmo_amd import ops
-from oracle import unet_ref as R
-rng = np.random.default_rng({H} + {W})
-N, H, W = 2, {H}, {W}
-x1 = rng.standard_normal((N, H, W, 32)).astype(np.float32)
-x2 = rng.standard_normal((N, H, W, 64)).astype(np.float32)
-w = (rng.standard_normal((64, 3, 3, 96)) * 0.1).astype(np.float32)
-b = rng.standard_normal(64).astype(np.float32)
-bf = lambda a: torch.tensor(a).to(torch.bfloat16)
-wf = torch.empty(w.size, dtype=torch.bfloat16, device="cuda")
-ops.prep_conv3x3(1, torch.tensor(w).cuda(), 64, 96, wf, None)
-v1 = ops.View(bf(x1).cuda().reshape(-1), N, H, W, 32, 32)
-v2 = ops.View(bf(x2).cuda().reshape(-1), N, H, W, 64, 64)
-out = ops.new_view(N, H, W, 64, torch.bfloat16)
-rows = ops.conv3x3_stat_rows(1, N, H, W, 96, 64)
-st = torch.zeros(rows * 128, device="cuda")
-ops.conv3x3_fwd_cat(1, v1, v2, wf, torch.tensor(b).cuda(), out, 1 | 2, stats=st)
-torch.cuda.synchronize()
-xc = np.concatenate([bf(x1).double().numpy(), bf(x2).double().numpy()], 3)
-ref = np.maximum(R.conv2d_same(xc, bf(w).double().numpy(), b), 0)
-got = out.buf.float().cpu().numpy().reshape(ref.shape)
-err = float(np.abs(got - ref).max()) / max(1.0, float(np.abs(ref).max()))
-s = st.view(rows, 2, 64).double().sum(0).cpu().numpy()
-serr = float(np.abs(s[0] - got.reshape(-1, 64).sum(0)).max()) / max(1.0, float(np.abs(got).sum()))
-print("kernel", ops.query("cnnitmo_conv3x3_kernel_name", 1, N, H, W, 96, 64, 0).decode(), "err", err, "serr", serr)
-assert err <= 1.5e-2 and serr <= 1e-5
-"""
-    env = dict(os.environ, CNNITMO_HALO_TH8=th8)
-    r = subprocess.run([_sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    print(r.stdout.strip().splitlines()[-1])
+def test_conv3x3_fwd_cat_dec9(H, W):
+    """cnnitmo_conv3x3_fwd_cat on dec9's shape ([conv1 32 | up9 64] -> 64, model.py:261-262)
+    vs the oracle on the materialised concat: ReLU + BN sums (16-row tiles, the two
+    members read per 32-channel chunk)."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(H + W)
+    N = 2
+    x1 = rng.standard_normal((N, H, W, 32)).astype(np.float32)
+    x2 = rng.standard_normal((N, H, W, 64)).astype(np.float32)
+    w = (rng.standard_normal((64, 3, 3, 96)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(64).astype(np.float32)
+    wf = torch.empty(w.size, dtype=torch.bfloat16, device="cuda")
+    ops.prep_conv3x3(1, torch.tensor(w).cuda(), 64, 96, wf, None)
+    v1 = ops.View(dev(x1, "bf16").reshape(-1), N, H, W, 32, 32)
+    v2 = ops.View(dev(x2, "bf16").reshape(-1), N, H, W, 64, 64)
+    out = ops.new_view(N, H, W, 64, torch.bfloat16)
+    rows = ops.conv3x3_stat_rows(1, N, H, W, 96, 64)
+    st = torch.zeros(rows * 128, device="cuda")
+    ops.conv3x3_fwd_cat(1, v1, v2, wf, torch.tensor(b).cuda(), out, 1 | 2, stats=st)
+    torch.cuda.synchronize()
+    xc = np.concatenate([rnd(x1, "bf16"), rnd(x2, "bf16")], 3).astype(np.float64)
+    ref = np.maximum(R.conv2d_same(xc, rnd(w, "bf16").astype(np.float64), b), 0)
+    got = host(out.buf).reshape(ref.shape)
+    err = float(np.abs(got - ref).max()) / max(1.0, float(np.abs(ref).max()))
+    s = st.view(rows, 2, 64).double().sum(0).cpu().numpy()
+    serr = float(np.abs(s[0] - got.reshape(-1, 64).sum(0)).max()) / max(1.0, float(np.abs(got).sum()))
+    assert err <= 1.5e-2 and serr <= 1e-5, (err, serr)

@@ -50,10 +50,9 @@ def label(name):
     n = unmangle(name.replace(" ", "")).replace("(anonymousnamespace)::", "")
     m = re.search(r"halo_conv_kernel<(?:(__bf16|float),)?(\d+),(\d+)(?:,(true|false))?(?:,(true|false))?(?:,(\d+))?(?:,(?:true|false))?>", n)
     if m:
-        return "halo_conv_kernel<%s%s,%s%s%s%s>" % ("f32," if m.group(1) == "float" else "", m.group(2), m.group(3),
-                                                   ",wres" if m.group(4) == "true" else "",
-                                                   ",pool" if m.group(5) == "true" else "",
-                                                   ",th8" if m.group(6) == "8" else "")
+        pool = "" if m.group(5) != "true" else (",route" if m.group(3) == "2" else ",pool")
+        return "halo_conv_kernel<%s%s,%s%s%s>" % ("f32," if m.group(1) == "float" else "", m.group(2), m.group(3),
+                                                 ",wres" if m.group(4) == "true" else "", pool)
     m = re.search(r"halo_gemm_kernel<(\d+),(\d+),(\d+),(\d+),\d+(?:,(\d+))?>", n)
     if m:
         return "halo_gemm_kernel<%s,%s,%s,%s%s>" % (m.groups()[:4] + (",bnb" if m.group(5) not in (None, "0") else "",))
