@@ -370,6 +370,26 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       for (int j = 0; j < 8; ++j) gr[j] = 0.f;
     }
   };
+  // EPI 2 (bf16): r of the tile (and the routed pool gradient) for the fused BN backward.
+  // EARLY (32-column blocks, whose registers have room for them): issued at the start of
+  // the tile's last item, so that item's MFMAs cover their HBM latency; otherwise after the
+  // MFMAs (the BN-64 kernels sit at 256 VGPRs).
+#ifndef HALO_EARLY_R
+#define HALO_EARLY_R 1
+#endif
+  constexpr bool EARLY = EPI == 2 && ES == 2 && FP == 1 && HALO_EARLY_R;
+  constexpr int NEARLY = FM * FP + (POOL && EPI == 2 ? 2 * FMR * FP : 0);  // loads per wave
+  dma::i32x4 rv[EPI == 2 && ES == 2 ? FM : 1][EPI == 2 && ES == 2 ? FP : 1];
+  auto load_r16 = [&](const Pos& e) {
+    if constexpr (EPI == 2 && ES == 2) {
+      const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int q = 0; q < FP; ++q) rv[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r_off(e, f, q), 0, 0);
+      load_route(e);
+    }
+  };
   auto compute = [&](int buf, bool pf, int ch) {
     const char* Ps = smem + buf * STAGE;
     const char* Bs = RES ? smem + C::WRES + ch * (C::BPC * 1024) : Ps + C::PATCH;
@@ -597,25 +617,21 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // dz or g by column (global stores; out-of-image pixels go to the sink).  bf16: g is
   // rounded to bf16 first (as cnnitmo_bn_bwd_apply reads it from a bf16 buffer); fp32:
   // r of one column pair at a time (two 16-byte pieces per (pixel, 8 channels)).
-  auto epilogue_bnb16 = [&](const Pos& e) {
+  auto epilogue_bnb16 = [&](const Pos& e, int npost) {
     const int oh0 = e.y0 + wave * RPW;
     const int c0 = p.bnb_c0, c1 = p.bnb_c1, cbn = c1 - c0;
     const long m0 = ((long)e.img * p.ho + oh0) * p.wo + e.x0;  // the wave's first pixel
-    dma::i32x4 rv[FM][FP];
-    {
-      const __amdgpu_buffer_rsrc_t rs = dma::brsrc(r_base(e));
-#pragma unroll
-      for (int f = 0; f < FM; ++f)
-#pragma unroll
-        for (int q = 0; q < FP; ++q) rv[f][q] = __builtin_amdgcn_raw_buffer_load_b128(rs, r_off(e, f, q), 0, 0);
+    // (late loads: the wait also retires the next item's DMA, issued during this item's
+    // first taps.  Pulling these pieces into L2 one item ahead by LDS-DMA into the sink
+    // measured 15-25 % slower on every fused dgrad (dec6-dec8), whether issued before or
+    // after the ring's pieces.  Non-temporal r loads and epilogue stores (to keep the patch
+    // lines in L2 for the next chunk) measured 1-4 % slower on levels 0-2.)
+    if constexpr (EARLY) {
+      dma::wait_vm_dyn(npost);  // the early loads, not the npost younger DMA pieces
+    } else {
+      load_r16(e);
+      dma::wait_vm<0>();
     }
-    load_route(e);
-    // (also retires the next item's DMA, issued during this item's first taps).  Pulling
-    // these pieces into L2 one item ahead by LDS-DMA into the sink measured 15-25 %
-    // slower on every fused dgrad (dec6-dec8), whether issued before or after the
-    // ring's pieces.  Non-temporal r loads and epilogue stores (to keep the patch
-    // lines in L2 for the next chunk) measured 1-4 % slower on levels 0-2.
-    dma::wait_vm<0>();
     bf16* __restrict__ O = (bf16*)p.out;
     bf16* __restrict__ Z = (bf16*)p.bnb_out;
 #pragma unroll
@@ -742,8 +758,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     zero_acc();
   };
 
-  auto epilogue_bnb = [&](const Pos& e) {
-    if constexpr (ES == 2) epilogue_bnb16(e);
+  auto epilogue_bnb = [&](const Pos& e, int npost) {
+    if constexpr (ES == 2) epilogue_bnb16(e, npost);
     else epilogue_bnb32(e);
   };
 
@@ -784,6 +800,12 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     __builtin_amdgcn_sched_barrier(0);
     const bool pf = t + ST - 1 < T;
     if (pf) issue_prep(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
+    if constexpr (EARLY) {
+      if (ep.ch == nch - 1) {  // the tile's last item: its epilogue's loads go out now
+        load_r16(ep);
+        issued += NEARLY;
+      }
+    }
     const bool act = ep.y0 + wave * RPW < p.ho;
     if (act) {
       compute(buf, pf, ep.ch);  // issues those loads between its taps
@@ -797,7 +819,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       mq[ST - 1] = issued;
     }
     if (ep.ch == nch - 1) {
-      if constexpr (EPI == 2) epilogue_bnb(ep);
+      if constexpr (EPI == 2) epilogue_bnb(ep, pf ? L : 0);
       else epilogue(ep);
       issued += NST;
     }
@@ -923,6 +945,13 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   // pooled forward: BN sums (training, BN folded: r stored) or the affine (inference), not both
   if (a.pool_out && (a.flags & CNNITMO_STATS) && (a.flags & CNNITMO_AFFINE)) return false;
   pl.bn = a.N % 64 == 0 ? 64 : (a.N % 32 == 0 ? 32 : 0);
+  // the routed-pool dgrad (EPI 2 + POOL): 32-column blocks by default, whose epilogue keeps the
+  // pooled gradient and indices in registers without spilling (CNNITMO_ROUTE_BN=64: 64 columns)
+  static const int route_bn = [] {
+    const char* e = getenv("CNNITMO_ROUTE_BN");
+    return e ? atoi(e) : 32;
+  }();
+  if (a.pool_out && a.bnb_out && route_bn == 32 && a.N % 32 == 0) pl.bn = 32;
   if (!pl.bn || a.N / pl.bn > halo_ncu() / 8) return false;
   if (a.bnb_out) {  // fused BN backward (input gradient)
     if (a.bnb_c0 % 8 || a.bnb_c1 % 8 || a.bnb_c0 < 0 || a.bnb_c1 > a.N || a.bnb_c0 >= a.bnb_c1 ||

@@ -445,7 +445,7 @@ class BlockStage(Stage):
             return None
         for m, ci0 in targets:
             if m.fuse_into is self and m.sum_consumers == 1:
-                if self.kind == "c3" and self._split_fused(ci0, m.c):
+                if self.kind == "c3" and self._split_fused(ci0, m.c, n):
                     rows = ops.conv3x3_dgrad_bn_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, m.c, 0, m.c)
                 elif self.kind == "c3":
                     rows = ops.conv3x3_dgrad_bn_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, self.cin, ci0,
@@ -476,7 +476,8 @@ class BlockStage(Stage):
         launched here but inside conv1's BN backward, where pool1's gradient is routed in
         (cnnitmo_conv3x3_dgrad_bn_pooled): the 32-channel skip gradient is neither written
         nor read back, and the stand-alone pooled BN-backward apply disappears.
-        CNNITMO_DEFER_SKIP=0: the separate dgrad + bn_bwd_apply_pooled."""
+        CNNITMO_DEFER_SKIP=0: the separate dgrad + bn_bwd_apply_pooled; =dec9: dec9 only.
+        (_split_fused splits dec7's and dec8's input gradients for the same purpose.)"""
         e = self.eng
         if os.environ.get("CNNITMO_DEFER_SKIP", "1") == "0" or not e.fuse_bnb:
             return False
@@ -488,13 +489,22 @@ class BlockStage(Stage):
             return False
         return ops.conv3x3_dgrad_bn_pooled_rows(e.dt, n, self.vout.h, self.vout.w, self.cout, skip.c) > 0
 
-    def _split_fused(self, ci0, c):
-        """dec9's input gradient (concat [skip 32 | up 64], model.py:261): two launches
-        -- the skip columns as a plain 32-column dgrad and the up columns as a 64-column
-        dgrad with the fused BN backward -- instead of one with 48-column blocks whose
-        epilogue straddles both (measured 15 ms).  CNNITMO_SPLIT_DGRAD=0: one launch."""
-        return (ci0 > 0 and ci0 + c == self.cin and self.cin % 64 != 0 and c % 64 == 0 and ci0 % 32 == 0
-                and os.environ.get("CNNITMO_SPLIT_DGRAD", "1") != "0")
+    def _split_fused(self, ci0, c, n):
+        """The input gradient of a concat consumer as two launches: the up columns [ci0, cin)
+        as a dgrad with the fused BN backward, and the skip columns [0, ci0) apart.
+        dec9 (concat [skip 32 | up 64], model.py:261): always -- one launch would need
+        48-column blocks whose epilogue straddles both (measured 15 ms); its skip part is a
+        plain dgrad, or deferred (_defer_skip).  dec7 / dec8 (model.py:251, 256): when the
+        skip member's gradient is deferred into its producer's BN backward with its pool's
+        route (CNNITMO_DEFER_SKIP=1; "dec9": dec9 only).  CNNITMO_SPLIT_DGRAD=0: one launch."""
+        if not (ci0 > 0 and ci0 + c == self.cin and ci0 % 32 == 0 and os.environ.get("CNNITMO_SPLIT_DGRAD", "1") != "0"):
+            return False
+        if self.cin % 64 != 0 and c % 64 == 0:
+            return True
+        if os.environ.get("CNNITMO_DEFER_SKIP", "1") != "1":
+            return False
+        skip = self._skip_member(ci0)
+        return skip is not None and self._defer_skip(skip, n)
 
     def _weight_and_input_grads(self, n, P, par, dz, part2, rows):
         e = self.eng
@@ -559,7 +569,7 @@ class BlockStage(Stage):
             prod = m.producer
             coef = prod.bn_coef(n)
             whole = ci0 == 0 and m.c == self.cin
-            split = self.kind == "c3" and self._split_fused(ci0, m.c)
+            split = self.kind == "c3" and self._split_fused(ci0, m.c, n)
             skip = self._skip_member(ci0) if split else None
             dx = None
             if not whole:

@@ -83,6 +83,21 @@ def _im2col(xp, kh, kw, H, W, h0, h1):
     return cols.reshape(N, h1 - h0, W, kh * kw * C)
 
 
+def _bands(H, band, fn):
+    """fn(h0, h1) over the row bands [h0, h1) of H, results in band order.  Large frames run
+    the bands on a thread pool (numpy releases the GIL in the im2col copies and in BLAS);
+    every band's arithmetic is the same as in a sequential loop."""
+    spans = [(h0, min(H, h0 + band)) for h0 in range(0, H, band)]
+    if len(spans) < 4:
+        return [fn(a, b) for a, b in spans]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=_POOL) as ex:
+        return list(ex.map(lambda s: fn(*s), spans))
+
+
+_POOL = max(1, min(8, int(__import__("os").environ.get("OMP_NUM_THREADS", "8") or 8)))
+
+
 def conv2d_same(x, w, b=None, band=64):
     """Conv2D 'same', stride 1.  x [N,H,W,Ci], w OHWI [Co,kh,kw,Ci], b [Co]."""
     N, H, W, Ci = x.shape
@@ -91,10 +106,10 @@ def conv2d_same(x, w, b=None, band=64):
     xp = np.pad(x, ((0, 0), (ph, ph), (pw, pw), (0, 0)))
     wm = w.reshape(Co, -1).T  # [kh*kw*Ci, Co]
     out = np.empty((N, H, W, Co), dtype=x.dtype)
-    for h0 in range(0, H, band):
-        h1 = min(H, h0 + band)
-        cols = _im2col(xp, kh, kw, H, W, h0, h1)
-        out[:, h0:h1] = cols @ wm
+
+    def one(h0, h1):
+        out[:, h0:h1] = _im2col(xp, kh, kw, H, W, h0, h1) @ wm
+    _bands(H, band, one)
     if b is not None:
         out += b
     return out
@@ -108,10 +123,10 @@ def conv2d_same_bwd(x, w, dz, need_dx=True, band=64):
     db = dz.reshape(-1, Co).sum(0)
     xp = np.pad(x, ((0, 0), (ph, ph), (pw, pw), (0, 0)))
     dw = np.zeros((kh * kw * Ci, Co), dtype=x.dtype)
-    for h0 in range(0, H, band):
-        h1 = min(H, h0 + band)
-        cols = _im2col(xp, kh, kw, H, W, h0, h1).reshape(-1, kh * kw * Ci)
-        dw += cols.T @ dz[:, h0:h1].reshape(-1, Co)
+    parts = _bands(H, band, lambda h0, h1: _im2col(xp, kh, kw, H, W, h0, h1).reshape(-1, kh * kw * Ci).T
+                   @ dz[:, h0:h1].reshape(-1, Co))
+    for pt in parts:  # summed in band order, as a sequential loop would
+        dw += pt
     dw = dw.T.reshape(Co, kh, kw, Ci)
     dx = None
     if need_dx:
@@ -136,13 +151,21 @@ def tconv2x2s2(x, k, b=None):
 
 
 def tconv2x2s2_bwd(x, k, dout):
+    """dx[n,h,w,i] = sum_{a,b,O} dout[n,2h+a,2w+b,O] k[a,b,O,i];  dk[a,b,O,i] = sum_{n,h,w}
+    dout[n,2h+a,2w+b,O] x[n,h,w,i] -- one GEMM per tap (a, b)."""
     N, H, W, Ci = x.shape
     Co = k.shape[2]
     d = dout.reshape(N, H, 2, W, 2, Co)
-    dx = np.einsum("nhawbO,abOi->nhwi", d, k, optimize=True)
-    dk = np.einsum("nhawbO,nhwi->abOi", d, x, optimize=True)
+    x2 = x.reshape(-1, Ci)
+    dx = np.zeros((N * H * W, Ci), dtype=np.result_type(dout, k))
+    dk = np.empty((2, 2, Co, Ci), dtype=np.result_type(dout, x))
+    for a in range(2):
+        for b in range(2):
+            dt = np.ascontiguousarray(d[:, :, a, :, b, :]).reshape(-1, Co)
+            dx += dt @ k[a, b]
+            dk[a, b] = dt.T @ x2
     db = dout.reshape(-1, Co).sum(0)
-    return dx, dk, db
+    return dx.reshape(N, H, W, Ci), dk, db
 
 
 # --------------------------------------------------------------------------

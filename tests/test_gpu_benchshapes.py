@@ -72,11 +72,12 @@ def _run(h, w, batch, dtype, train, expect):
 
 
 # MaxPooling2D at levels 0-2 rides on its producer's epilogue (conv3x3_fwd_pool, its BN-backward
-# sums from the pooled r: pool_bnsums_pooled); pool4 reads the Dropout output: maxpool_fwd
+# sums from the pooled r: pool_bnsums_pooled), and its backward on the deferred skip-path dgrad
+# of the concat consumer (conv3x3_dgrad_bn_pooled); pool4 reads the Dropout output: maxpool_fwd
 TRAIN = ["conv_c3_fwd", "conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_cat", "conv_wgrad_cat", "tconv_fwd",
          "conv3x3_dgrad", "conv3x3_dgrad_bn", "conv3x3_dgrad_bn_pooled", "tconv_dgrad", "tconv_dgrad_bn", "conv_wgrad", "tconv_wgrad",
          "conv_c3_wgrad", "maxpool_fwd", "maxpool_bwd", "pool_bnsums_pooled", "bn_fwd_finalize", "bn_apply", "bn_bwd_reduce",
-         "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_pooled", "bn_bwd_apply_g3", "bn_consumer_sums", "colsum",
+         "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_g3", "bn_consumer_sums", "colsum",
          "border_sums", "head_fwd_bwd_g3", "head_finalize", "rmsprop", "prep_conv3x3", "prep_tconv", "prep_c3",
          "fold_conv3x3", "fold_tconv"]
 # predict(): conv9's second conv computes the sigmoid head in its epilogue (conv3x3_fwd_head)
