@@ -69,9 +69,12 @@ def main():
         row = {"dispatches": int(c["SQ_WAVE_CYCLES"][1]), "wave_cycles_per_dispatch": wc}
         for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
             row[k + "/WAVE"] = m(k) / wc
-        busy = m("SQ_VALU_MFMA_BUSY_CYCLES") / (m("GRBM_GUI_ACTIVE") / XCDS * SIMDS)
+        mb = m("SQ_VALU_MFMA_BUSY_CYCLES")
+        if not mb or mb != mb:
+            continue  # (no matrix work: not a conv kernel)
+        busy = mb / (m("GRBM_GUI_ACTIVE") / XCDS * SIMDS)
         row["mfma_busy_frac"] = busy
-        row["coexec/mfma_busy"] = m("SQ_VALU_MFMA_COEXEC_CYCLES") / m("SQ_VALU_MFMA_BUSY_CYCLES")
+        row["coexec/mfma_busy"] = m("SQ_VALU_MFMA_COEXEC_CYCLES") / mb
         # pass 2 is another run of the same launches: normalise by its own GRBM cycles
         g2 = None
         for k in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM",
