@@ -67,7 +67,8 @@ def parse():
     ap.add_argument("--k4-warmup", type=int, default=3)
     ap.add_argument("--f32-train-batch", type=int, default=8,
                     help="fp32 1080p training leg (the reference's Keras precision) frames per GPU; 0 = skip")
-    ap.add_argument("--f32-train-steps", type=int, default=5)
+    ap.add_argument("--f32-train-steps", type=int, default=10)
+    ap.add_argument("--f32-train-warmup", type=int, default=3)
     ap.add_argument("--ns-batch", type=int, default=32,
                     help="north-star leg: fp32 1080p inference (conv2d forward) at this batch per GPU; 0 = skip")
     return ap.parse_args()
@@ -89,9 +90,9 @@ class KernelTimer:
 
     @staticmethod
     def fwd_name(dt, n):
-        """Kernel chosen by igemm_fwd.hip's dispatch for n GEMM columns (mirrors pick2/use_v1)."""
+        """Kernel chosen by igemm_fwd.hip's dispatch for n GEMM columns (mirrors pick2)."""
         t = "bf16" if dt == 1 else "f32"
-        if n == 32 or os.environ.get("CNNITMO_FWD_V1") == "1":
+        if n == 32:
             return f"igemm_fwd_kernel<{t},256x32>"
         bn = 128 if n % 128 == 0 else 64 if n % 64 == 0 else 96 if n % 96 == 0 else 32
         return f"igemm_fwd2_kernel<{t},256x{bn}>"
@@ -562,21 +563,22 @@ def main():
     def guarded(fn, *a):
         ok = True
         try:
-            return fn(*a)
+            res = fn(*a)
         except Exception as e:
             ok = False
             import traceback
             traceback.print_exc()
-            return {"error": repr(e)[:500]}
+            res = {"error": repr(e)[:500]}
         finally:
             timer.on = False
             timer.rec = []
             C.clear_session()
             torch.cuda.empty_cache()
-            try:
-                agree(ok)
-            except RuntimeError:
-                pass
+        try:
+            agree(ok)
+        except RuntimeError:  # this rank's leg succeeded, another rank's failed: the leg failed
+            res = {"error": "leg failed on another rank"}
+        return res
 
     # configs[1]: fp32 inference leg (b8 1080p, BN moving stats), same ranks, weak
     infer = ns = k4 = f32t = None
@@ -618,6 +620,12 @@ def main():
         if infer is not None:
             line["fp32_infer"] = infer
         if ns is not None:
+            cb = (infer or {}).get("cpu_baseline") if isinstance(infer, dict) else None
+            if isinstance(ns, dict) and ns.get("cpu_baseline") is None and cb and "value" in cb:
+                # the oracle's fp32 inference rate is per frame, whatever the GPU batch: the
+                # configs[1] leg's timing of the same forward, on the same host in this run
+                ns["cpu_baseline"] = dict(cb, sample=cb.get("sample", "") + "; the fp32_infer leg's timing "
+                                          "(frames/s of the same per-frame forward; the batch is a GPU-side choice)")
             line["fp32_infer_b32"] = ns
         if k4 is not None:
             line["k4_train"] = k4
@@ -812,7 +820,8 @@ def f32_train_leg(args, rank, world, timer, barrier, agree, cpu_1080):
     """The reference's own training precision (Keras fp32, main.py:126-132) at 1080p:
     fp32 storage and fp32 MFMA (16x16x4 f32), f32_train_batch frames per GPU."""
     return train_leg(args, rank, world, timer, barrier, agree, cpu_1080, args.height, args.width,
-                     args.f32_train_batch, "float32", args.f32_train_steps, 2, "fp32 training, main.py:126-132")
+                     args.f32_train_batch, "float32", args.f32_train_steps, args.f32_train_warmup,
+                     "fp32 training, main.py:126-132")
 
 
 if __name__ == "__main__":

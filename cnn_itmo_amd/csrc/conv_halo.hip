@@ -952,6 +952,14 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
     return e ? atoi(e) : 32;
   }();
   if (a.pool_out && a.bnb_out && route_bn == 32 && a.N % 32 == 0) pl.bn = 32;
+  // fused BN-backward dgrads with at most this many columns on 32-column blocks (their r
+  // loads then go out early); all of them measured 3 % slower on the bench step
+  // (profiles/r05/r05e_ab_bnb_bn32.txt)
+  static const int bnb32 = [] {
+    const char* e = getenv("CNNITMO_BNB_BN32");
+    return e ? atoi(e) : 0;
+  }();
+  if (a.bnb_out && a.N <= bnb32 && a.N % 32 == 0) pl.bn = 32;
   if (!pl.bn || a.N / pl.bn > halo_ncu() / 8) return false;
   if (a.bnb_out) {  // fused BN backward (input gradient)
     if (a.bnb_c0 % 8 || a.bnb_c1 % 8 || a.bnb_c0 < 0 || a.bnb_c1 > a.N || a.bnb_c0 >= a.bnb_c1 ||

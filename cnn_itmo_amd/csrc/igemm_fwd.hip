@@ -283,19 +283,11 @@ int launch_fwd(FwdArgs a, hipStream_t s, const char* what) {
   return cnnitmo_check_launch(what);
 }
 
-bool use_v1() {
-  static const bool v1 = [] {
-    const char* e = getenv("CNNITMO_FWD_V1");
-    return e && atoi(e) == 1;
-  }();
-  return v1;
-}
-
 int dispatch(int dtype, const FwdArgs& a, void* stream, const char* what) {
   hipStream_t s = (hipStream_t)stream;
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return launch_halo(a, s, what);
   if (dtype == CNNITMO_F32 && halo_handles(a, true)) return launch_halo(a, s, what, true);
-  if (!use_v1() && fwd2_handles(a.N)) {
+  if (fwd2_handles(a.N)) {
     if (dtype == CNNITMO_BF16) return launch_fwd2<bf16>(a, s, what);
     if (dtype == CNNITMO_F32) return launch_fwd2<float>(a, s, what);
   }
@@ -353,7 +345,7 @@ extern "C" long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int c
 
 extern "C" int cnnitmo_fwd_stat_rows(int dtype, long m, int ncols) {
   (void)dtype;
-  if (!use_v1() && fwd2_handles(ncols)) return fwd2_stat_rows(m);
+  if (fwd2_handles(ncols)) return fwd2_stat_rows(m);
   Cfg c = pick_cfg(ncols);
   return (int)((m + c.bm - 1) / c.bm);
 }
@@ -507,7 +499,7 @@ extern "C" const char* cnnitmo_conv3x3_kernel_name(int dtype, int n, int h, int 
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
   if (dtype == CNNITMO_F32 && halo_handles(a, true)) return halo_name(a, true);  // (no BN sums: inference)
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
-  if (!use_v1() && fwd2_handles(a.N)) {
+  if (fwd2_handles(a.N)) {
     const int bn = a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
     snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,%dx%d>", t, fwd2_bm(a, dtype == CNNITMO_BF16), bn);
   } else {
@@ -536,7 +528,7 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
   static thread_local char buf[96];
   const char* t = dtype == CNNITMO_BF16 ? "bf16" : "f32";
-  if (!use_v1() && fwd2_handles(a.N)) {
+  if (fwd2_handles(a.N)) {
     const bool t256 = fwd2_t256(a, dtype == CNNITMO_BF16);
     const int bn = t256 ? 256 : a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
     const int bm = t256 ? 256 : fwd2_bm(a, dtype == CNNITMO_BF16);

@@ -411,17 +411,8 @@ void launch_any(const WgradArgs& a, int bm, int bn, hipStream_t s, dim3 grid) {
 #undef CNN_W
 }
 
-bool wgrad_v1() {
-  static const bool v1 = [] {
-    const char* e = getenv("CNNITMO_WGRAD_V1");
-    return e && atoi(e) == 1;
-  }();
-  return v1;
-}
-
 // bf16: the v2 kernel (igemm_wgrad2.hip); returns splits written, < 0 if not taken.
 int try_wgrad2(const WgradArgs& a, int tapdep, void* ws, size_t ws_bytes, hipStream_t s) {
-  if (wgrad_v1()) return -1;
   Wgrad2Args b;
   memset(&b, 0, sizeof(b));
   b.a = (const bf16*)a.a; b.a_ld = a.a_ld; b.a_off = a.a_off; b.ha = a.ha; b.wa = a.wa; b.a_scale = a.a_scale;
@@ -472,7 +463,7 @@ template <typename T>
 size_t ws_bytes_for(long P, int M, int N, int ntaps) {
   Plan pl = make_plan<T>(P, M, N, ntaps);
   size_t b = (size_t)pl.splits * M * N * ntaps * 4;
-  if (std::is_same<T, bf16>::value && !wgrad_v1()) b = std::max(b, wgrad2_ws_bytes(P, M, N, ntaps));
+  if (std::is_same<T, bf16>::value) b = std::max(b, wgrad2_ws_bytes(P, M, N, ntaps));
   return b;
 }
 
@@ -666,7 +657,7 @@ extern "C" const char* cnnitmo_wgrad_kernel_name(int dtype, int ntaps, int n, in
   }
   const long P = (long)n * h * w;
   static thread_local char buf[80];
-  if (dtype == CNNITMO_BF16 && !wgrad_v1()) {
+  if (dtype == CNNITMO_BF16) {
     const W2Label l = wgrad2_label(P, cout, cin, ntaps);
     if (l.ok) {
       snprintf(buf, sizeof(buf), "igemm_wgrad2_kernel<%d,%d,tpb%d>", l.bm, l.bn, l.tpb);

@@ -186,8 +186,7 @@ class BlockStage(Stage):
             self.w_bwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
         self.foldable = self.kind != "c3in" and self.vin.folded
         # first layer without im2col (32 filters; CNNITMO_C3_DIRECT=0: im2col + 1-tap GEMM):
-        # bf16 always (conv_c3 forward and weight gradient); fp32 for inference forwards
-        # (the fp32 weight gradient still reads im2col columns, so fp32 training packs them)
+        # both dtypes run conv_c3's forward and weight gradient, training and inference
         self.direct_ok = (self.kind == "c3in" and cout == 32 and os.environ.get("CNNITMO_C3_DIRECT", "1") != "0")
         self.direct = self.direct_ok
         if self.foldable:  # per-step folded copies (training)
@@ -251,6 +250,13 @@ class BlockStage(Stage):
         else:
             ops.tconv_fwd(e.dt, self.vin.view(n), self.w_fwd, bias, out_view, flags, aff, stats)
 
+    def _head_fits(self, n):
+        """The fused head addresses yhat [n][h_valid][w][3] fp32 with 32-bit offsets
+        (cnnitmo_conv3x3_fwd_head); a larger batch takes the unfused conv + head_fwd path,
+        whose head kernel only needs fewer than 2^31 pixels (e.g. fp32 4K at the default
+        Model.predict batch of 32)."""
+        return n * self.eng.h_valid * self.vout.w * 12 < (1 << 31)
+
     def _conv_head(self, n):
         """predict(): this conv with the sigmoid head in its epilogue, straight into the
         prediction buffer (cnnitmo_conv3x3_fwd_head); the conv's own output is never stored."""
@@ -298,7 +304,7 @@ class BlockStage(Stage):
         self.fold_active = training and self.foldable
         self.direct = self.direct_ok
         self.head_ran = False
-        if not training and self.head is not None and e._yhat is not None:
+        if not training and self.head is not None and e._yhat is not None and self._head_fits(n):
             self._conv_head(n)
             self.head_ran = True
             return
@@ -936,7 +942,7 @@ class Engine:
         [conv1 32 | up9 64] (model.py:261) puts 64 + 128 B of each 192-B row in lines
         shared with the neighbouring pixels, so the pool, its BN-sum pass and enc1b's
         BN-backward apply read conv1 in half lines and up9 writes them.  Its consumer
-        (dec9a, a 3x3 conv) then reads both members directly: cnnitmo_conv3x3_fwd_cat /
+        (conv9, a 3x3 conv, model.py:261) then reads both members directly: cnnitmo_conv3x3_fwd_cat /
         cnnitmo_conv_wgrad_cat (bf16 halo kernels; its input gradient is already split
         per member).  CNNITMO_SPLIT_CAT=0, or sizes either entry point rejects: one
         concat buffer."""
@@ -993,8 +999,8 @@ class Engine:
             st.vout.coef_src = v
 
     def _plan_head_fusion(self):
-        """The sigmoid head (model.py:264) into the inference epilogue of the 3x3 ConvBN that
-        feeds it (conv9's second conv): predict() then never stores that conv's 64-channel
+        """The sigmoid head (model.py:276) into the inference epilogue of the 3x3 ConvBN that
+        feeds it (conv9, model.py:261): predict() then never stores that conv's 64-channel
         output (fp32 b8 at 1080p: 4.3 GB written and read back).  Needs: a 'c3' producer with
         BN and no Dropout / pooling / concat, consumed by the head alone, 64 channels, the halo
         kernel for its sizes.  CNNITMO_HEAD_FUSE=0: the stand-alone head kernel."""

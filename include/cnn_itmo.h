@@ -89,8 +89,8 @@ int cnnitmo_conv3x3_fwd_pool(int dtype, const void* x, int x_ld, int x_off, int 
                              int flags, const float* aff_scale, const float* aff_shift, float* stat_part,
                              const float* border, void* pool_out, int pool_ld, unsigned char* pool_idx,
                              const float* pool_sign, void* stream);
-/* The last 3x3 ConvBN (model.py:262-263, conv9's second conv) with the sigmoid head
- * (model.py:264, Conv2D(3, 1, activation='sigmoid')) in its epilogue, for inference
+/* The last 3x3 ConvBN (conv9 = ConvBN(64, 3, merge9), model.py:261) with the sigmoid head
+ * (model.py:276, Conv2D(3, 1, activation='sigmoid')) in its epilogue, for inference
  * (predict.py:62): yhat [n][h_valid][w][3] fp32 = sigmoid(y . head_w[3][cout] + head_b), y = the
  * conv's epilogue output (flags/aff as cnnitmo_conv3x3_fwd: ReLU, BN affine), never stored.
  * Replaces cnnitmo_conv3x3_fwd + cnnitmo_head_fwd.  cout = 64; no BN sums. */
@@ -196,7 +196,7 @@ int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
  * the uncorrected sum dz (x) r, input of cnnitmo_bn_consumer_sums. */
 
 /* cnnitmo_conv_wgrad (ntaps 9, bf16) over concatenate([x1, x2]) read from its members
- * (see cnnitmo_conv3x3_fwd_cat): c1 == 32, cin == 96 (dec9a, model.py:261-262).
+ * (see cnnitmo_conv3x3_fwd_cat): c1 == 32, cin == 96 (conv9, model.py:260-261).
  * workspace: cnnitmo_wgrad_cat_workspace_bytes (0 = unsupported sizes). */
 size_t cnnitmo_wgrad_cat_workspace_bytes(int n, int h, int w, int c1, int cin, int cout);
 const char* cnnitmo_wgrad_cat_kernel_name(int n, int h, int w, int c1, int cin, int cout);

@@ -160,3 +160,17 @@ def test_lds_swizzles_conflict_free():
     assert cs.check_b128()
     for R in (32, 64, 96, 128):
         assert cs.check_tr(R), R
+
+
+def test_fused_head_size_fallback():
+    """predict's fused conv9 + head (cnnitmo_conv3x3_fwd_head) addresses yhat with 32-bit
+    offsets: batches whose fp32 yhat reaches 2 GiB take the unfused conv + head_fwd path
+    (BlockStage._head_fits), e.g. fp32 4K at Model.predict's default batch of 32."""
+    from types import SimpleNamespace
+    from cnn_itmo_amd.engine import BlockStage
+    st = SimpleNamespace(eng=SimpleNamespace(h_valid=2160), vout=SimpleNamespace(w=3840))
+    assert BlockStage._head_fits(st, 21)          # 21 * 2160 * 3840 * 12 B < 2^31
+    assert not BlockStage._head_fits(st, 22)
+    assert not BlockStage._head_fits(st, 32)
+    st = SimpleNamespace(eng=SimpleNamespace(h_valid=1080), vout=SimpleNamespace(w=1920))
+    assert BlockStage._head_fits(st, 86) and not BlockStage._head_fits(st, 87)

@@ -80,7 +80,7 @@ TRAIN = ["conv_c3_fwd", "conv3x3_fwd", "conv3x3_fwd_pool", "conv3x3_fwd_cat", "c
          "bn_bwd_finalize", "bn_bwd_apply", "bn_bwd_apply_g3", "bn_consumer_sums", "colsum",
          "border_sums", "head_fwd_bwd_g3", "head_finalize", "rmsprop", "prep_conv3x3", "prep_tconv", "prep_c3",
          "fold_conv3x3", "fold_tconv"]
-# predict(): conv9's second conv computes the sigmoid head in its epilogue (conv3x3_fwd_head)
+# predict(): conv9 (model.py:261) computes the sigmoid head (model.py:276) in its epilogue (conv3x3_fwd_head)
 INFER_F32 = ["prep_conv3x3", "prep_tconv", "prep_c3", "conv_c3_fwd", "conv3x3_fwd", "conv3x3_fwd_pool", "tconv_fwd",
              "maxpool_fwd", "bn_infer_coeffs", "conv3x3_fwd_head"]
 
