@@ -21,7 +21,7 @@ DROPOUT = 1
 NO_BN = 2
 PARITY = 4
 BIAS_PER_COL = 8
-CONSUMER_ROWS = 16
+CONSUMER_ROWS = 64
 
 vp = C.c_void_p
 i32 = C.c_int

@@ -377,6 +377,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 #ifndef HALO_EARLY_R
 #define HALO_EARLY_R 1
 #endif
+
   constexpr bool EARLY = EPI == 2 && ES == 2 && FP == 1 && HALO_EARLY_R;
   constexpr int NEARLY = FM * FP + (POOL && EPI == 2 ? 2 * FMR * FP : 0);  // loads per wave
   dma::i32x4 rv[EPI == 2 && ES == 2 ? FM : 1][EPI == 2 && ES == 2 ? FP : 1];

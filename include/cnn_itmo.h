@@ -379,7 +379,7 @@ int cnnitmo_bn_bwd_apply_g3(int dtype, const float* g3, const float* wh, const v
  * part has CNNITMO_CONSUMER_ROWS rows [rows][2][c].  cnnitmo_pool_bnsums adds a
  * MaxPooling2D consumer's share (dyp: the pooled gradient; r: the pool input's
  * view; rows = cnnitmo_bn_bwd_rows(n*(h/2)*(w/2), c)). */
-#define CNNITMO_CONSUMER_ROWS 16
+#define CNNITMO_CONSUMER_ROWS 64
 int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* raw, int cout, int cin_tot, int ci0,
                              int c, const float* db, const float* vtab, const float* mean,
                              const float* invstd, float* part, void* stream);

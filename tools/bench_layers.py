@@ -23,7 +23,10 @@ LAYERS = [
     ("enc4b", "c3", 3, 256, 256), ("crossa", "c3", 4, 256, 512), ("crossb", "c3", 4, 512, 512),
     ("up6", "t2", 4, 512, 512), ("dec6", "c3", 3, 768, 512), ("up7", "t2", 3, 512, 256),
     ("dec7", "c3", 2, 384, 256), ("up8", "t2", 2, 256, 128), ("dec8", "c3", 1, 192, 128),
-    ("up9", "t2", 1, 128, 64), ("dec9", "c3", 0, 96, 64), ("dec9b", "c3", 0, 64, 64),
+    ("up9", "t2", 1, 128, 64), ("dec9", "c3", 0, 96, 64),
+    # conv9's input gradient for its up9 columns alone (the split launch, engine._split_fused:
+    # dz 64 channels -> the 64 columns of up9), as a 64 -> 64 shape; not a layer of its own
+    ("dec9up", "c3", 0, 64, 64),
 ]
 
 
@@ -92,7 +95,7 @@ def main():
                 # decoder dgrad with the up-path producer's BN backward fused (engine: concat
                 # [skip, up], up = the tconv output at channels [cin - cout, cin), parity sums);
                 # a level-0 conv whose whole input is the previous conv's BN output: [0, cin)
-                par = name.startswith("dec") and name != "dec9b"
+                par = name.startswith("dec") and name != "dec9up"
                 c0, c1 = (cin - cout, cin) if par else (0, cin)
                 dx = ops.new_view(B, h, w, cin, T)
                 r = ops.View(x.buf, B, h, w, c1 - c0, cin, c0)
