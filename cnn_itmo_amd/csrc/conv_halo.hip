@@ -946,21 +946,13 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
   // pooled forward: BN sums (training, BN folded: r stored) or the affine (inference), not both
   if (a.pool_out && (a.flags & CNNITMO_STATS) && (a.flags & CNNITMO_AFFINE)) return false;
   pl.bn = a.N % 64 == 0 ? 64 : (a.N % 32 == 0 ? 32 : 0);
-  // the routed-pool dgrad (EPI 2 + POOL): 32-column blocks by default, whose epilogue keeps the
-  // pooled gradient and indices in registers without spilling (CNNITMO_ROUTE_BN=64: 64 columns)
-  static const int route_bn = [] {
-    const char* e = getenv("CNNITMO_ROUTE_BN");
-    return e ? atoi(e) : 32;
-  }();
-  if (a.pool_out && a.bnb_out && route_bn == 32 && a.N % 32 == 0) pl.bn = 32;
-  // fused BN-backward dgrads with at most this many columns on 32-column blocks (their r
-  // loads then go out early); all of them measured 3 % slower on the bench step
-  // (profiles/r05/r05e_ab_bnb_bn32.txt)
-  static const int bnb32 = [] {
-    const char* e = getenv("CNNITMO_BNB_BN32");
-    return e ? atoi(e) : 0;
-  }();
-  if (a.bnb_out && a.N <= bnb32 && a.N % 32 == 0) pl.bn = 32;
+  // the routed-pool dgrad (EPI 2 + POOL): 32-column blocks, whose epilogue keeps the pooled
+  // gradient and indices in registers without spilling (64-column blocks measured 0.3 %
+  // slower on the bench step, profiles/r05/r05c_ab_route_bn64.txt).  The other fused BN-backward
+  // dgrads keep 64 columns: 32-column blocks, whose r loads can go out early, measured 3 %
+  // slower for all of them and 1 % for those up to 64 columns (r05e_ab_bnb_bn32.txt,
+  // r05h_ab_bnb_bn32_64.txt)
+  if (a.pool_out && a.bnb_out && a.N % 32 == 0) pl.bn = 32;
   if (!pl.bn || a.N / pl.bn > halo_ncu() / 8) return false;
   if (a.bnb_out) {  // fused BN backward (input gradient)
     if (a.bnb_c0 % 8 || a.bnb_c1 % 8 || a.bnb_c0 < 0 || a.bnb_c1 > a.N || a.bnb_c0 >= a.bnb_c1 ||

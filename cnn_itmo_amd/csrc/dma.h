@@ -44,6 +44,16 @@ __device__ __forceinline__ void lds16(unsigned voff, i32x4 rs, const char* lds) 
                "s"(a) : "memory");
 }
 
+// the same with a wave-uniform byte offset added in the SGPR slot (not range-checked:
+// voff alone decides whether the piece is in range)
+// (LDS destination as a 32-bit LDS address: no generic-pointer conversion per piece)
+__device__ __forceinline__ void lds16s(unsigned voff, i32x4 rs, unsigned soff, unsigned lds) {
+  const unsigned a = __builtin_amdgcn_readfirstlane(lds);
+  const unsigned so = __builtin_amdgcn_readfirstlane(soff);
+  asm volatile("s_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds" ::"v"(voff), "s"(rs),
+               "s"(so), "s"(a) : "memory");
+}
+
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }

@@ -176,27 +176,44 @@ extern "C" int cnnitmo_bn_infer_coeffs(int c, const float* gamma, const float* b
   return cnnitmo_check_launch("bn_infer_coeffs");
 }
 
-// y view = r*scale + shift [+ Dropout(0.5)].  One thread = one 16-byte vector.
+// y view = r*scale + shift [+ Dropout(0.5)].  One thread = one 16-byte vector.  lg >= 0:
+// C / VE = 2^lg and fewer than 2^31 vectors, so the (pixel, channel) split of a vector index
+// is a shift and a mask in 32 bits (the 64-bit division cost as much as the hash).
 template <typename T>
 __global__ void bn_apply_kernel(const T* __restrict__ r, long P, int C, const float* __restrict__ sc,
                                 const float* __restrict__ sh, T* __restrict__ y, long y_ld, int y_off,
-                                int drop, uint64_t dbase) {
+                                int drop, uint64_t dbase, int lg) {
   constexpr int VE = Vec16<T>::N;
   const int cv = C / VE;
   const long total = P * cv;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
-       i += (long)gridDim.x * blockDim.x) {
-    const long p = i / cv;
-    const int c0 = (int)(i - p * cv) * VE;
-    float v[VE];
+  auto one = [&](long p, int c0) {
+    float v[VE], a[VE], b[VE];
     Pack16<T>::load(r + (size_t)p * C + c0, v);
 #pragma unroll
+    for (int e = 0; e < VE; e += 4) {
+      const float4 s4 = *reinterpret_cast<const float4*>(sc + c0 + e), h4 = *reinterpret_cast<const float4*>(sh + c0 + e);
+      a[e] = s4.x; a[e + 1] = s4.y; a[e + 2] = s4.z; a[e + 3] = s4.w;
+      b[e] = h4.x; b[e + 1] = h4.y; b[e + 2] = h4.z; b[e + 3] = h4.w;
+    }
+    const uint64_t i0 = (uint64_t)p * C + c0;
+#pragma unroll
     for (int e = 0; e < VE; ++e) {
-      float o = v[e] * sc[c0 + e] + sh[c0 + e];
-      if (drop) o = dropout_keep(dbase, (uint64_t)p * C + c0 + e) ? o * 2.f : 0.f;
+      float o = v[e] * a[e] + b[e];
+      if (drop) o = dropout_keep(dbase, i0 + e) ? o * 2.f : 0.f;
       v[e] = o;
     }
     Pack16<T>::store(y + (size_t)p * y_ld + y_off + c0, v);
+  };
+  if (lg >= 0) {
+    const unsigned tot = (unsigned)total, msk = (unsigned)cv - 1u;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x)
+      one((long)(i >> lg), (int)(i & msk) * VE);
+    return;
+  }
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total;
+       i += (long)gridDim.x * blockDim.x) {
+    const long p = i / cv;
+    one(p, (int)(i - p * cv) * VE);
   }
 }
 
@@ -207,12 +224,15 @@ extern "C" int cnnitmo_bn_apply(int dtype, const void* r, long p, int c, const f
   const int drop = (flags & CNNITMO_DROPOUT) ? 1 : 0;
   const uint64_t base = dropout_base(drop_seed, (uint64_t)drop_layer);
   CNN_REQUIRE(c % 8 == 0 && y_ld % 8 == 0 && y_off % 8 == 0, "bn_apply: channels must be multiples of 8");
+  CNN_REQUIRE((uintptr_t)scale % 16 == 0 && (uintptr_t)shift % 16 == 0, "bn_apply: scale/shift must be 16-byte aligned");
+  const int ve = dtype == CNNITMO_BF16 ? 8 : 4, cv = c / ve;
+  const int lg = ((cv & (cv - 1)) == 0 && p * cv < (1L << 31)) ? __builtin_ctz((unsigned)cv) : -1;
   if (dtype == CNNITMO_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(grid_for(p * c / 8)), dim3(256), 0, s,
-                       (const bf16*)r, p, c, scale, shift, (bf16*)y, (long)y_ld, y_off, drop, base);
+                       (const bf16*)r, p, c, scale, shift, (bf16*)y, (long)y_ld, y_off, drop, base, lg);
   else
     hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(grid_for(p * c / 4)), dim3(256), 0, s,
-                       (const float*)r, p, c, scale, shift, (float*)y, (long)y_ld, y_off, drop, base);
+                       (const float*)r, p, c, scale, shift, (float*)y, (long)y_ld, y_off, drop, base, lg);
   return cnnitmo_check_launch("bn_apply");
 }
 

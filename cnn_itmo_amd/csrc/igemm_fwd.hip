@@ -523,7 +523,14 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
   a.N = dgrad ? cin : 4 * cout;
   a.a_ld = a.cin; a.out_ld = dgrad ? cin : cout; a.cout = cout;
   a.scatter = dgrad ? 0 : 1;
-  if (dgrad) { a.ntaps = 4; a.scale = 2; a.hs = 2 * h; a.ws = 2 * w; }
+  if (dgrad) {
+    a.ntaps = 4; a.scale = 2; a.hs = 2 * h; a.ws = 2 * w;
+    a.dyc = a.dxc = 0;
+    for (int t = 0; t < 4; ++t) {  // (as cnnitmo_tconv2x2_dgrad)
+      a.dyc |= ((t >> 1) + 1) << (2 * t);
+      a.dxc |= ((t & 1) + 1) << (2 * t);
+    }
+  }
   a.M = (long)n * h * w;
   if (dtype == CNNITMO_BF16 && halo_handles(a)) return halo_name(a);
   static thread_local char buf[96];
@@ -532,7 +539,10 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
     const bool t256 = fwd2_t256(a, dtype == CNNITMO_BF16);
     const int bn = t256 ? 256 : a.N % 128 == 0 ? 128 : a.N % 64 == 0 ? 64 : a.N % 96 == 0 ? 96 : 32;
     const int bm = t256 ? 256 : fwd2_bm(a, dtype == CNNITMO_BF16);
-    snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,%dx%d>", t, bm, bn);
+    if (fwd2_pers(a, dtype == CNNITMO_BF16))
+      snprintf(buf, sizeof(buf), "igemm_fwd2p_kernel<%s,%dx%d>", t, bm, bn);
+    else
+      snprintf(buf, sizeof(buf), "igemm_fwd2_kernel<%s,%dx%d>", t, bm, bn);
   } else {
     const Cfg c = pick_cfg(a.N);
     snprintf(buf, sizeof(buf), "igemm_fwd_kernel<%s,%dx%d>", t, c.bm, c.bn);

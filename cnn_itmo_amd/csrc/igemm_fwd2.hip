@@ -18,8 +18,10 @@
 // LDS image: [rows][128 B], 16-byte chunk c of row r at slot c ^ ((r >> 1) & 7):
 // conflict-free for the fragment reads (lane l: row l&15, chunk 4*kk + (l>>4))
 // in every ds_read_b128 bank group (derivation in DESIGN.md).
+#include <algorithm>
 #include <cstdlib>
 
+#include "dma.h"
 #include "igemm_common.h"
 
 __device__ __attribute__((aligned(256))) unsigned char g_zero_page[256] = {0};
@@ -290,6 +292,172 @@ __global__ __launch_bounds__(WM * WN * 64) void igemm_fwd2_kernel(const FwdArgs 
 }
 
 // ----------------------------------------------------------------------------
+// Persistent form of the 256 x 256 bf16 launch, for the Conv2DTranspose input gradient
+// (up6 / up7, K = 4 taps x Cout; a plain store epilogue: it issues no loads, so it never
+// waits on the next tile's ring DMA).  One workgroup per CU walks
+// its XCD's contiguous tile range (XCD x owns tiles [T*x/8, T*(x+1)/8); its Gx workgroups
+// take every Gx-th tile, so the XCD's resident tiles are consecutive: both column blocks
+// of a row block share the A rows in that XCD's L2).  The ring runs across tile
+// boundaries: the next tile's first K-step is loaded during the current tile's last one,
+// so a tile has no prologue bubble.  The MFMA runs with the operands swapped (C^T) on
+// pair_perm'd weight rows, so each lane holds 8 consecutive output channels of one pixel
+// and the epilogue is 16-byte buffer stores straight from the accumulators (no LDS C tile,
+// no barrier): FM * FN / 2 stores per wave per tile, issued unconditionally (rows past M
+// get an out-of-range offset and are dropped) so the next K-step's counted wait is exact.
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void igemm_fwd2p_kernel(const FwdArgs p) {
+  using C = Fwd2Cfg<bf16, BM, BN, WM, WN, 2>;
+  constexpr int VE = C::VE, KE = C::KE, TM = C::TM, TN = C::TN, FM = C::FM, FN = C::FN;
+  constexpr int NA = C::NA, NB = C::NB, STAGE = C::STAGE;
+  constexpr int NS = FM * FN / 2;  // epilogue stores per wave per tile
+  static_assert(FN % 2 == 0 && TN % 32 == 0, "column pairs");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int T = p.mblocks * p.nblocks;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, gx = gridDim.x >> 3;
+  const int q8 = T >> 3, r8 = T & 7;
+  const int tbeg = xcd * q8 + (xcd < r8 ? xcd : r8), tcnt = q8 + (xcd < r8 ? 1 : 0);
+  if (slot >= tcnt) return;  // (whole workgroup: no barrier reached)
+  const int nmine = (tcnt - slot + gx - 1) / gx;
+  const int K = p.ntaps * p.cin;
+  const int nk = (K + KE - 1) / KE;
+  const int S = nmine * nk;
+  const bf16* __restrict__ A = (const bf16*)p.a;
+  const bf16* __restrict__ B = (const bf16*)p.b;
+  const long hw = (long)p.ho * p.wo;
+
+  // ---- issue side: the tile whose K-steps are being loaded ----------------------
+  // Every K-step lies inside one tap (cin % KE == 0) and every tap is in range (source
+  // grid = 2 x the iteration grid), so a piece's address is a per-tile lane offset (its
+  // row's source pixel and chunk) plus a wave-uniform per-step offset (tap, channel) in
+  // the buffer instruction's SGPR slot: no address arithmetic per load.
+  const int sub = lane >> 3, pslot = lane & 7;
+  const int cA0 = pslot ^ (sub >> 1), cA1 = cA0 ^ 4;
+  unsigned voa[NA], vob[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    vob[i] = (unsigned)(((long)pair_perm((wave * NB + i) * 8 + sub) * K + ((i & 1) ? cA1 : cA0) * VE) * 2);
+  const long pix_ld = p.a_ld * 2;  // bytes per source pixel
+  const unsigned hw32 = (unsigned)hw, wo32 = (unsigned)p.wo;
+  dma::i32x4 ra, rb;
+  int i_k = 0, i_j = 0, i_tap = 0, i_ch = 0;
+  auto set_issue = [&](int j) {  // j-th tile of this workgroup
+    const int tile = tbeg + slot + j * gx;
+    const int mb = tile / p.nblocks;
+    const unsigned m0 = (unsigned)mb * BM;
+    const unsigned img0 = m0 / hw32, r0 = m0 - img0 * hw32, oh0 = r0 / wo32;
+    const long p0 = ((long)img0 * p.hs + 2 * oh0) * p.ws + 2 * (r0 - oh0 * wo32);
+    ra = dma::rsrc((uintptr_t)(A + p0 * p.a_ld + p.a_off));
+    rb = dma::rsrc((uintptr_t)(B + (size_t)(tile - mb * p.nblocks) * BN * K));
+    // source pixel of row m relative to row m0's: 2 x (its iteration-grid offset), each
+    // iteration row spanning 2 source rows (image boundaries included: hs = 2 ho)
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const unsigned d = (wave * NA + i) * 8 + sub, m = m0 + d;
+      const unsigned rows = (r0 % wo32 + d) / wo32, col = (r0 % wo32 + d) - rows * wo32;
+      const unsigned px = rows * 2 * (unsigned)p.ws + 2 * col - 2 * (r0 % wo32);
+      voa[i] = m < (unsigned)p.M ? px * (unsigned)pix_ld + ((i & 1) ? cA1 : cA0) * VE * 2 : dma::OOB;
+    }
+    i_k = i_tap = i_ch = 0;
+  };
+  auto advance = [&]() {
+    if (++i_k == nk) {
+      if (++i_j < nmine) set_issue(i_j);
+      return;
+    }
+    i_ch += KE;
+    if (i_ch == p.cin) { i_ch = 0; ++i_tap; }
+  };
+  const unsigned lds0 = dma::lds_addr(smem);
+  auto issue = [&](int buf) {
+    const unsigned As = lds0 + buf * STAGE, Bs = As + BM * 128;
+    const unsigned sa = (unsigned)((((i_tap >> 1) * p.ws + (i_tap & 1)) * pix_ld) + i_ch * 2);
+    const unsigned sb = (unsigned)(i_k * KE * 2);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) dma::lds16s(voa[i], ra, sa, As + (wave * NA + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dma::lds16s(vob[i], rb, sb, Bs + (wave * NB + i) * 1024);
+  };
+
+  f32x4 acc[FM][FN];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero();
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 128;
+    const int frow = lane & 15, fg = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      uint4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const uint4*>(As + swz_off(wm * TM + i * 16 + frow, kk * 4 + fg));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const uint4*>(Bs + swz_off(wn * TN + j * 16 + frow, kk * 4 + fg));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], bfr[j], af[i]);  // C^T
+    }
+  };
+  auto epilogue = [&](int j) {
+    const int tile = tbeg + slot + j * gx;
+    const int mb = tile / p.nblocks;
+    const long m0 = (long)mb * BM;
+    const int n0 = (tile - mb * p.nblocks) * BN;
+    const __amdgpu_buffer_rsrc_t os = dma::brsrc((const bf16*)p.out + m0 * p.out_ld + p.out_off + n0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int row = wm * TM + i * 16 + (lane & 15);
+      const bool ok = m0 + row < p.M;
+#pragma unroll
+      for (int q = 0; q < FN / 2; ++q) {
+        const int c = wn * TN + 32 * q + 8 * (lane >> 4);
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = (bf16)acc[i][2 * q + (k >> 2)][k & 3];
+        const unsigned off = (unsigned)(((long)row * p.out_ld + c) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, o), os, ok ? off : dma::OOB, 0, 0);
+      }
+    }
+  };
+
+  // ---- main loop: one flat K-step sequence over this workgroup's tiles ---------------
+  set_issue(0);
+  issue(0);
+  advance();
+  int ck = 0, cj = 0;  // compute side: K-step within tile, tile
+  bool stored = false;
+  for (int g = 0; g < S; ++g) {
+    if (stored) dma::wait_vm<NS>(); else dma::wait_vm<0>();  // (the stores were issued after the loads)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + 1 < S) {
+      issue((g + 1) & 1);
+      advance();
+    }
+    compute(g & 1);
+    stored = false;
+    if (++ck == nk) {
+      epilogue(cj);
+      zero();
+      ck = 0;
+      ++cj;
+      stored = true;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
 namespace {
 struct Cfg2 {
   int bn;
@@ -353,6 +521,28 @@ bool fwd2_t256(const FwdArgs& a, bool bf16) {
   return en && bf16 && a.ntaps == 4 && a.scale == 2 && a.N % 256 == 0 && !a.stats;
 }
 
+// ... as the persistent kernel (igemm_fwd2p_kernel) for the input-gradient geometry when
+// nothing is asked of the epilogue but the store; CNNITMO_FWD2_PERS=0: the one-tile-per-workgroup launch
+bool fwd2_pers(const FwdArgs& a, bool bf16) {
+  static const int en = [] {
+    const char* e = getenv("CNNITMO_FWD2_PERS");
+    return e ? atoi(e) : 1;
+  }();
+  return en && fwd2_t256(a, bf16) && !a.scatter && !a.border && !a.bias && !a.flags &&
+         a.hs == 2 * a.ho && a.ws == 2 * a.wo && a.cin % 64 == 0 && a.dyc == 0xa5 && a.dxc == 0x99 && !a.cin1 && a.M < (1L << 31) &&
+         (2L * (256 / a.wo + 2) + 2) * a.ws * a.a_ld * 2 < (1L << 31);  // (a tile's source span: 32-bit offsets)
+}
+
+static int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return v;
+  }();
+  return n;
+}
+
 template <typename T>
 int launch_fwd2(FwdArgs a, hipStream_t s, const char* what) {
   constexpr int VE = Vec16<T>::N;
@@ -364,6 +554,16 @@ int launch_fwd2(FwdArgs a, hipStream_t s, const char* what) {
   CNN_REQUIRE(a.M > 0 && a.ntaps >= 1 && a.ntaps <= 9, "%s: bad sizes", what);
   const Cfg2 c = pick2(a.N);
   if constexpr (sizeof(T) == 2) {
+    if (fwd2_pers(a, true)) {
+      a.mblocks = (int)((a.M + 255) / 256);
+      a.nblocks = a.N / 256;
+      const long t = (long)a.mblocks * a.nblocks;
+      CNN_REQUIRE(t < (1L << 31), "%s: grid too large", what);
+      CNN_REQUIRE((long)256 * a.out_ld * 2 + (long)a.N * 2 < (1L << 31), "%s: output row too wide", what);
+      const long g = 8 * std::min((long)std::max(cu_count() / 8, 1), (t + 7) / 8);  // one per CU, 8 | grid
+      hipLaunchKernelGGL((igemm_fwd2p_kernel<256, 256, 2, 4>), dim3((unsigned)g), dim3(512), 0, s, a);
+      return cnnitmo_check_launch(what);
+    }
     if (fwd2_t256(a, true)) {
       a.mblocks = (int)((a.M + 255) / 256);
       a.nblocks = a.N / 256;

@@ -386,20 +386,8 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
   // K = 256 or 512: the row padding below is conflict-free (K % 128 == 0) and the K loop
   // is compiled for K / 32 = 8 or 16 steps (a multiple of TWS_PD)
   if (K != 256 && K != 512) return false;
-  static const int bn256 = [] {
-    const char* e = getenv("CNNITMO_TWS_BN256");
-    return e ? atoi(e) : 0;
-  }();
-  // forward at K = 256 (up8): a 256-column block (two taps of 128 channels) with 16-pixel
-  // wave tiles, so every pixel row is read by 2 column blocks instead of 4.  Off by
-  // default: 2.45 -> 2.28 ms with 64-byte store segments, but 2.33 against BN 128's 2.01-2.06
-  // once the stores write whole lines (profiles/r03y_ab_bn256.txt, r03z_ab_lines_bn256.txt)
-  if (bn256 && mode == 0 && K == 256 && cout == 128 && N % 256 == 0) {
-    pl.bn = 256;
-    pl.nblk = N / 256;
-    pl.gpx = 32 / pl.nblk;
-    return true;
-  }
+  // (a 256-column forward block at K = 256 (up8), 16-pixel wave tiles: 2.33 ms against BN
+  // 128's 2.01-2.06 once the stores write whole lines, profiles/r03z_ab_lines_bn256.txt)
   int bn = 128;
   while (bn >= 64 && (long)bn * (K * 2 + WS_PAD) + 3 * bn * 4 > 148 * 1024) bn /= 2;
   if (bn < 64 || N % bn) return false;
@@ -436,7 +424,7 @@ const char* tconv_ws_name(int mode, int cin, int cout, bool f32) {
   WSPlan pl;
   if (!ws_plan(mode, cin, cout, pl, f32)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "tconv_ws_kernel<%s%d,%d>", f32 ? "f32," : "", mode, pl.bn);  // (bn 256: 16-pixel tiles)
+  snprintf(buf, sizeof(buf), "tconv_ws_kernel<%s%d,%d>", f32 ? "f32," : "", mode, pl.bn);
   return buf;
 }
 
@@ -457,7 +445,7 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
   t.out = out; t.out_ld = out_ld; t.out_off = out_off;
   t.bias = bias; t.flags = flags; t.aff_scale = aff_scale; t.aff_shift = aff_shift; t.stats = stats;
   t.nblk = pl.nblk; t.gpx = pl.gpx;
-  const int tp = pl.bn == 256 ? 16 : 32;  // pixels per wave tile
+  const int tp = 32;  // pixels per wave tile
   t.tiles = ((long)n * h * w + tp - 1) / tp;
   const int grid = 8 * pl.gpx * pl.nblk;  // 256: one workgroup per CU
   const size_t lds = (size_t)pl.bn * (t.K * (f32 ? 4 : 2) + WS_PAD) + 3 * pl.bn * sizeof(float);
@@ -466,7 +454,6 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 256, 8, 1, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 64, 32, 2, 2, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -483,8 +470,6 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
     if (t.K == 512) hipLaunchKernelGGL((tconv_ws_kernel<0, 64, 32, 2, 2, float>), dim3(grid), dim3(NW * 64), lds, s, t);
     else if (t.K == 256) hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 16, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
     else hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 8, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
-  } else if (pl.bn == 256) {
-    hipLaunchKernelGGL((tconv_ws_kernel<0, 256, 8, 1, 4>), dim3(grid), dim3(NW * 64), lds, s, t);
   } else if (mode == 0) {
     if (t.K == 256) TWL(0, 8);
     else TWL(0, 16);

@@ -143,9 +143,12 @@ def test_conv_affine_inference_epilogue(dt, H, W):
                                           # bf16 weight-stationary kernel: fwd at 32 column blocks
                                           # (512 -> 512), dgrad at BN 128 (256 <- 128); ragged tiles
                                           (512, 512, 3, 7), (256, 128, 7, 9),
-                                          # 1024 / 2048-deep gradients (up7 / up6: igemm_fwd2's
-                                          # 256 x 256 tiles; ragged tiles)
+                                          # 1024 / 2048-deep gradients (up7 / up6: igemm_fwd2p's
+                                          # persistent 256 x 256 tiles; ragged tiles)
                                           (512, 256, 5, 7), (512, 256, 17, 33), (256, 512, 9, 31),
+                                          # > 256 tiles of 256 x 256: each persistent workgroup
+                                          # (igemm_fwd2p_kernel, one per CU) walks several
+                                          (512, 256, 96, 176),
                                           # bf16 row-streaming wgrad: 4 rows per workgroup, 2 strips
                                           (512, 512, 16, 40)])
 def test_tconv(dt, cin, cout, H, W):
@@ -297,10 +300,11 @@ def test_maxpool_ties(dt):
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("drop", [False, True])
-def test_bn_train_fwd_bwd(dt, drop):
+@pytest.mark.parametrize("C", [64, 96])  # (96: bn_apply's generic, non-power-of-two index path)
+def test_bn_train_fwd_bwd(dt, drop, C):
     from cnn_itmo_amd import ops
     rng = np.random.default_rng(5)
-    N, H, W, C = 2, 5, 7, 64
+    N, H, W = 2, 5, 7
     P = N * H * W
     r = np.maximum(rng.standard_normal((N, H, W, C)), 0).astype(np.float32)
     g = rng.uniform(0.5, 1.5, C).astype(np.float32)

@@ -50,7 +50,7 @@ def test_train1080_fp32_step_vs_oracle():
     m.set_named_weights(P)
     eng = m._engine()
     la = eng.train_step(torch.tensor(x, dtype=torch.float32).cuda(), torch.tensor(t, dtype=torch.float32).cuda(),
-                        seed=SEED, apply=False).cpu().numpy()
+                        seed=SEED, apply=False).cpu().numpy().astype(np.float64)
     grads = eng.get_grads()
     after = m.named_weights()
     C.clear_session()

@@ -65,6 +65,9 @@ def label(name):
     m = re.search(r"wgrad_halo_kernel<(\d+),(\d+),(\d+),", n)
     if m:
         return "wgrad_halo_kernel<%s,%s,%s>" % m.groups()
+    m = re.search(r"igemm_fwd2p_kernel<(\d+),(\d+),", n)
+    if m:
+        return "igemm_fwd2p_kernel<bf16,%sx%s>" % m.groups()
     m = re.search(r"igemm_fwd2_kernel<__bf16,(\d+),(\d+),", n) or re.search(r"igemm_fwd2_kernel<[^,]*,(\d+),(\d+),", n)
     if m:
         t = "bf16" if "bf16" in n else "f32"
