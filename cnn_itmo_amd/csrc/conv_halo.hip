@@ -373,12 +373,12 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // EPI 2 (bf16): r of the tile (and the routed pool gradient) for the fused BN backward.
   // EARLY (32-column blocks, whose registers have room for them): issued at the start of
   // the tile's last item, so that item's MFMAs cover their HBM latency; otherwise after the
-  // MFMAs (the BN-64 kernels sit at 256 VGPRs).
-#ifndef HALO_EARLY_R
-#define HALO_EARLY_R 1
-#endif
-
-  constexpr bool EARLY = EPI == 2 && ES == 2 && FP == 1 && HALO_EARLY_R;
+  // MFMAs (the BN-64 kernels sit at 256 VGPRs).  Early vs late on the 32-column kernels:
+  // 215.4 / 215.4 vs 215.4 / 213.9 frames/s (profiles/r05/r05d_ab_early_r.txt).
+  // (Single-buffered fragments on the 64-column kernels, which frees the registers for early
+  // r loads: every 64-column fused dgrad 8-27 % slower, 218.0 -> 212.2 frames/s,
+  // profiles/r05/r05q_ab_sb64_early_r.txt.)
+  constexpr bool EARLY = EPI == 2 && ES == 2 && FP == 1;
   constexpr int NEARLY = FM * FP + (POOL && EPI == 2 ? 2 * FMR * FP : 0);  // loads per wave
   dma::i32x4 rv[EPI == 2 && ES == 2 ? FM : 1][EPI == 2 && ES == 2 ? FP : 1];
   auto load_r16 = [&](const Pos& e) {
@@ -799,7 +799,13 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    const bool pf = t + ST - 1 < T;
+#ifndef HALO_PROBE_NODMA  // timing probes (tools/build_variant.sh): no DMA after the prologue /
+#define HALO_PROBE_NODMA 0  // no forward epilogue; results are garbage
+#endif
+#ifndef HALO_PROBE_NOEPI
+#define HALO_PROBE_NOEPI 0
+#endif
+    const bool pf = t + ST - 1 < T && !HALO_PROBE_NODMA;
     if (pf) issue_prep(buf == 0 ? ST - 1 : buf - 1);  // stage (t + ST - 1) % ST
     if constexpr (EARLY) {
       if (ep.ch == nch - 1) {  // the tile's last item: its epilogue's loads go out now
@@ -819,7 +825,15 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       issued += L;
       mq[ST - 1] = issued;
     }
-    if (ep.ch == nch - 1) {
+    if (ep.ch == nch - 1 && HALO_PROBE_NOEPI && EPI == 1) {  // (probe: the accumulators stay live)
+      float z = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) z += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      if (p.flags == 0x7fff0000) ((float*)p.out)[lane] = z;
+      zero_acc();
+    } else if (ep.ch == nch - 1) {
       if constexpr (EPI == 2) epilogue_bnb(ep, pf ? L : 0);
       else epilogue(ep);
       issued += NST;
