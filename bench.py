@@ -287,8 +287,8 @@ def _host_info():
 
 
 def cpu_baseline(args, P_init, H, W, train=True):
-    """Time the numpy oracle (fp32, OpenBLAS sgemm, all BLAS threads) on ONE frame at
-    (H/s, W/s): a training step (fwd+bwd) or an inference forward; report
+    """Time the numpy oracle (fp32, OpenBLAS sgemm, the box's CPU share) on ONE frame at
+    (H/s, W/s): a training step (fwd+bwd) or an inference forward, repeated to >= 10 s; report
     1080p-frame-equivalents per second (FLOPs scale with pixel count)."""
     from oracle import unet_ref as R
     s = args.cpu_scale
@@ -298,27 +298,36 @@ def cpu_baseline(args, P_init, H, W, train=True):
     x = (rng.integers(0, 256, size=(1, h, w, 3)) / 255.0).astype(np.float32)
     t = (rng.integers(0, 256, size=(1, h, w, 3)) / 255.0).astype(np.float32)
     net = R.UNetRef(P_init, np.float32)
-    t0 = time.perf_counter()
-    net.forward(x, training=train, seed=0)
-    if train:
-        net.backward(t)
-    dt = time.perf_counter() - t0
     cores, blas, model = _host_info()
+    # the oracle runs its convs' row bands on R._POOL threads, each in BLAS: split the CPU share
+    # between them so that the threads in use never exceed it
+    per = max(1, blas // R._POOL)
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(limits=per, user_api="blas"):
+        k, t0 = 0, time.perf_counter()
+        while True:  # repeated to at least 10 s of CPU work
+            net.forward(x, training=train, seed=0)
+            if train:
+                net.backward(t)
+            k += 1
+            if time.perf_counter() - t0 >= 10.0:
+                break
+        dt = (time.perf_counter() - t0) / k
     frac = (h * w) / float(H * W)
     what = "train step (fwd+bwd)" if train else "inference forward (BN moving stats)"
     return {"value": frac / dt, "unit": "1080p frames/s (%s, fp32)" % ("fwd+bwd" if train else "fwd"),
-            "cores": blas, "kind": "port",
+            "cores": R._POOL * per, "kind": "port",
             "sample": f"oracle/unet_ref.py numpy fp32 {what} on 1 frame {w}x{h} "
-                      f"({frac:.4f} of a 1920x{H} frame, scaled by pixel count); {dt:.2f} s",
-            "seconds": dt, "padded_h": H, "affinity_cores": cores, "blas_threads": blas, "cpu_model": model,
-            "threads_note": THREADS_NOTE}
+                      f"({frac:.4f} of a 1920x{H} frame, scaled by pixel count), {k} x {dt:.2f} s",
+            "seconds": dt, "padded_h": H, "affinity_cores": cores, "blas_threads": per, "band_threads": R._POOL,
+            "cpu_model": model, "threads_note": THREADS_NOTE}
 
 
-# `cores` is the BLAS thread count actually used.  The GPU box allots 16 host CPUs per
-# GPU (the harness exports OMP_NUM_THREADS=16 and asks for pools of at most 16);
-# sched_getaffinity there lists every core of the host (256), which are not ours.
-THREADS_NOTE = ("BLAS threads = the box's CPU share per GPU (OMP_NUM_THREADS, 16 on the MI355X box); "
-                "affinity_cores counts the whole host")
+# `cores` is the thread count actually used.  The GPU box allots 16 host CPUs per GPU (the
+# harness exports OMP_NUM_THREADS=16 and asks for pools of at most 16); sched_getaffinity
+# there lists every core of the host (256), which are not ours.
+THREADS_NOTE = ("cores = the box's CPU share per GPU (OMP_NUM_THREADS, 16 on the MI355X box) = the oracle's "
+                "row-band threads x BLAS threads per band; affinity_cores counts the whole host")
 
 
 def cpu_config1():
