@@ -370,6 +370,9 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
     return e ? atoi(e) : 1;
   }();
   if (!en || cout % 32 || cin % 32) return false;
+  // the bf16 input gradient (up8, K = 512) runs on igemm_fwd2p_kernel: 1.52 -> 1.31 ms
+  // (profiles/r05/r05t2_ab_up8_dgrad_fwd2p.txt)
+  if (mode == 1 && !f32) return false;
   const int K = mode == 0 ? cin : 4 * cout, N = mode == 0 ? 4 * cout : cin;
   if (f32) {  // fp32 forward: the widest block whose fp32 rows fit (K 512: 64, 256 / 128: 128)
     // K = 128 is up9 (128 -> 64 channels at full resolution), which ran on igemm_fwd2's
@@ -395,10 +398,7 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
   if (nblk > 32 || 32 % nblk) return false;
   // where it measured faster than the halo / implicit-GEMM paths (tools/ab_env.sh,
   // b32 1080p): every forward at BN 128 (up6 1.50 -> 1.08, up7 2.62 -> 1.98, up8
-  // 3.16 -> 2.98 ms) and the gradient at BN 128 (up8: 2.48 -> 1.87 ms).  The up7
-  // gradient (K = 1024) needs BN 64: with 32-pixel tiles the A re-reads bound it, and
-  // with 64-pixel tiles (the same A loads per MFMA as BN 128) it measured 2.15 ms
-  // against igemm_fwd2's 1.90.
+  // 3.16 -> 2.98 ms).  (The bf16 input gradients moved to igemm_fwd2p_kernel, above.)
   if (bn != 128) return false;
   pl.bn = bn;
   pl.nblk = nblk;
@@ -452,8 +452,6 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
   static bool attr = [] {  // dynamic LDS beyond 64 KB
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<1, 128, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 64, 32, 2, 2, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 16, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)tconv_ws_kernel<0, 128, 8, 2, 4, float>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -470,12 +468,9 @@ int launch_tconv_ws(int mode, const void* a, long a_ld, int a_off, const void* b
     if (t.K == 512) hipLaunchKernelGGL((tconv_ws_kernel<0, 64, 32, 2, 2, float>), dim3(grid), dim3(NW * 64), lds, s, t);
     else if (t.K == 256) hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 16, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
     else hipLaunchKernelGGL((tconv_ws_kernel<0, 128, 8, 2, 4, float>), dim3(grid), dim3(NW * 64), lds, s, t);
-  } else if (mode == 0) {
+  } else {
     if (t.K == 256) TWL(0, 8);
     else TWL(0, 16);
-  } else {
-    if (t.K == 256) TWL(1, 8);
-    else TWL(1, 16);
   }
 #undef TWL
   return cnnitmo_check_launch(what);
