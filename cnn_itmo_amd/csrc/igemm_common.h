@@ -128,6 +128,10 @@ bool fwd2_handles(int N);  // v2 is the faster kernel for this column count
 int fwd2_bm(const FwdArgs& a, bool bf16);  // row tile of the v2 launch (128 or 256)
 bool fwd2_t256(const FwdArgs& a, bool bf16);  // 256 x 256 tiles (bf16 tconv input gradient)
 bool fwd2_pers(const FwdArgs& a, bool bf16);  // ... in the persistent kernel
+// the bf16 Conv2DTranspose forward in training, persistent (igemm_fwd2.hip)
+bool tfwd2p_handles(const FwdArgs& a, bool bf16);
+long tfwd2p_stat_rows(const FwdArgs& a);
+int launch_tfwd2p(FwdArgs a, hipStream_t s, const char* what);
 
 // halo-tiled 3x3 conv (bf16, 4x64 output tiles), conv_halo.hip
 bool halo_handles(const FwdArgs& a, bool f32 = false);  // f32: the fp32 forward / plain dgrad

@@ -330,9 +330,22 @@ extern "C" long cnnitmo_conv3x3_stat_rows(int dtype, int n, int h, int w, int ci
   return cnnitmo_fwd_stat_rows(dtype, a.M, cout);
 }
 
+// FwdArgs of cnnitmo_tconv2x2_fwd (dense in / out views) for the planners
+static FwdArgs tconv_fwd_args(int n, int h, int w, int cin, int cout, int flags) {
+  FwdArgs a = base_args();
+  a.nimg = n; a.hs = h; a.ws = w; a.ho = h; a.wo = w;
+  a.cin = cin; a.N = 4 * cout; a.a_ld = cin; a.out_ld = cout; a.M = (long)n * h * w;
+  a.scatter = 1; a.cout = cout; a.flags = flags;
+  return a;
+}
+
 extern "C" long cnnitmo_tconv2x2_stat_rows(int dtype, int n, int h, int w, int cin, int cout) {
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false))
     return tconv_stream_rows(0, n, h, w, cin, cout, false);
+  {
+    FwdArgs t = tconv_fwd_args(n, h, w, cin, cout, CNNITMO_RELU | CNNITMO_STATS);
+    if (dtype == CNNITMO_BF16 && tfwd2p_handles(t, true)) return tfwd2p_stat_rows(t);
+  }
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout)) return tconv_ws_rows(cin, cout);
   if (dtype == CNNITMO_F32 && tconv_ws_handles(0, cin, cout, true)) return tconv_ws_rows(cin, cout, true);
   FwdArgs a = base_args();
@@ -513,6 +526,9 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
                                                     int dgrad) {
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(dgrad ? 1 : 0, h, w, cin, cout, false))
     return tconv_stream_name(dgrad ? 1 : 0, h, w, cin, cout, false);
+  if (!dgrad && dtype == CNNITMO_BF16 &&
+      tfwd2p_handles(tconv_fwd_args(n, h, w, cin, cout, CNNITMO_RELU | CNNITMO_STATS), true))
+    return "tconv_fwd2p_kernel<bf16,256x256>";  // (the training forward; inference: tconv_ws)
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout))
     return tconv_ws_name(dgrad ? 1 : 0, cin, cout);
   if (dtype == CNNITMO_F32 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout, true))
@@ -683,6 +699,7 @@ extern "C" int cnnitmo_tconv2x2_fwd(int dtype, const void* x, int n, int h, int 
   if (dtype == CNNITMO_BF16 && tconv_stream_handles(0, h, w, cin, cout, false))
     return launch_tconv_stream(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
                                aff_shift, stat_part, nullptr, nullptr, 0, 0, (hipStream_t)stream, "tconv2x2_fwd");
+  if (dtype == CNNITMO_BF16 && tfwd2p_handles(a, true)) return launch_tfwd2p(a, (hipStream_t)stream, "tconv2x2_fwd");
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(0, cin, cout))
     return launch_tconv_ws(0, x, cin, 0, k, n, h, w, cin, cout, out, out_ld, out_off, bias, flags, aff_scale,
                            aff_shift, stat_part, (hipStream_t)stream, "tconv2x2_fwd");

@@ -457,6 +457,208 @@ __global__ __launch_bounds__(WM * WN * 64) void igemm_fwd2p_kernel(const FwdArgs
   }
 }
 
+// The same persistent walk for the Conv2DTranspose FORWARD in training (bf16, up6-up8):
+// C[m][n] = x[m] . K[n] with n = tap * Cout + co, bias + ReLU in the epilogue, each lane's 8
+// consecutive columns (one tap) stored as 16 bytes at output pixel (2i + tap/2, 2j + tap%2),
+// and the BN partial sums (sum v, sum v^2 of the stored values' fp32 precursors) kept in
+// registers for the whole launch.  For the sums to stay in registers a workgroup keeps ONE
+// column block: slot s of an XCD takes column block s % nblocks and every
+// (Gx/nblocks)-th row block of the XCD's contiguous row-block range (the nblocks
+// workgroups of a row block run side by side and share its x rows in L2).  Stats rows:
+// one per (XCD, slot / nblocks, wave row), every (row, column) written exactly once (a
+// workgroup without tiles writes zeros).
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs p) {
+  using C = Fwd2Cfg<bf16, BM, BN, WM, WN, 2>;
+  constexpr int VE = C::VE, KE = C::KE, TM = C::TM, TN = C::TN, FM = C::FM, FN = C::FN;
+  constexpr int NA = C::NA, NB = C::NB, STAGE = C::STAGE, FP = FN / 2;
+  constexpr int NS = FM * FP;  // epilogue stores per wave per tile
+  static_assert(FN % 2 == 0 && TN % 32 == 0, "column pairs");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + BN * 4];
+  float* bias_s = reinterpret_cast<float*>(smem + 2 * STAGE);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int frow = lane & 15, g = lane >> 4;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, gx = gridDim.x >> 3;
+  const int nb = slot % p.nblocks, s2 = slot / p.nblocks, gs = gx / p.nblocks;
+  const int q8 = p.mblocks >> 3, r8 = p.mblocks & 7;
+  const int mbeg = xcd * q8 + (xcd < r8 ? xcd : r8), mcnt = q8 + (xcd < r8 ? 1 : 0);
+  const int nmine = s2 < mcnt ? (mcnt - s2 + gs - 1) / gs : 0;
+  const int K = p.cin;
+  const int nk = K / KE;
+  const int S = nmine * nk;
+  const int n0 = nb * BN;
+  const bf16* __restrict__ A = (const bf16*)p.a;
+  const bf16* __restrict__ B = (const bf16*)p.b;
+  const unsigned hw32 = (unsigned)((long)p.ho * p.wo), wo32 = (unsigned)p.wo;
+  const bool relu = p.flags & CNNITMO_RELU, stats = p.flags & CNNITMO_STATS;
+  for (int i = tid; i < BN; i += WM * WN * 64) {
+    const int n = n0 + i;
+    bias_s[i] = !p.bias ? 0.f : p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : n - (n / p.cout) * p.cout];
+  }
+  // the lane's two 8-column groups: tap and channel (8 | cout: a group never straddles taps)
+  int tq[FP], cq[FP];
+#pragma unroll
+  for (int q = 0; q < FP; ++q) {
+    const int n = n0 + wn * TN + 32 * q + 8 * g;
+    tq[q] = n / p.cout;
+    cq[q] = n - tq[q] * p.cout;
+  }
+
+  const int sub = lane >> 3, pslot = lane & 7;
+  const int cA0 = pslot ^ (sub >> 1), cA1 = cA0 ^ 4;
+  unsigned voa[NA], vob[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    vob[i] = (unsigned)(((long)pair_perm((wave * NB + i) * 8 + sub) * K + ((i & 1) ? cA1 : cA0) * VE) * 2);
+  const dma::i32x4 rb = dma::rsrc((uintptr_t)(B + (size_t)n0 * K));
+  dma::i32x4 ra;
+  int i_k = 0, i_j = 0;
+  auto set_issue = [&](int j) {
+    const unsigned m0 = (unsigned)(mbeg + s2 + j * gs) * BM;
+    ra = dma::rsrc((uintptr_t)(A + (size_t)m0 * p.a_ld + p.a_off));
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const unsigned d = (wave * NA + i) * 8 + sub;
+      voa[i] = m0 + d < (unsigned)p.M ? (unsigned)((d * p.a_ld + ((i & 1) ? cA1 : cA0) * VE) * 2) : dma::OOB;
+    }
+    i_k = 0;
+  };
+  auto advance = [&]() {
+    if (++i_k == nk && ++i_j < nmine) set_issue(i_j);
+  };
+  const unsigned lds0 = dma::lds_addr(smem);
+  auto issue = [&](int buf) {
+    const unsigned As = lds0 + buf * STAGE, Bs = As + BM * 128;
+    const unsigned so = (unsigned)(i_k * KE * 2);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) dma::lds16s(voa[i], ra, so, As + (wave * NA + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dma::lds16s(vob[i], rb, so, Bs + (wave * NB + i) * 1024);
+  };
+
+  f32x4 acc[FM][FN];
+  auto zero = [&]() {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero();
+  float s1[FP][8], s2v[FP][8];
+#pragma unroll
+  for (int q = 0; q < FP; ++q)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s1[q][k] = s2v[q][k] = 0.f;
+  auto compute = [&](int buf) {
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + BM * 128;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      uint4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+        af[i] = *reinterpret_cast<const uint4*>(As + swz_off(wm * TM + i * 16 + frow, kk * 4 + g));
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        bfr[j] = *reinterpret_cast<const uint4*>(Bs + swz_off(wn * TN + j * 16 + frow, kk * 4 + g));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) Mma<bf16>::run(acc[i][j], bfr[j], af[i]);  // C^T
+    }
+  };
+  const float invw = 1.f / (float)p.wo;
+  const long out_px = (long)p.out_ld * 2;  // bytes per output pixel
+  auto epilogue = [&](int j) {
+    const unsigned m0 = (unsigned)(mbeg + s2 + j * gs) * BM;
+    const unsigned img0 = m0 / hw32, r0 = m0 - img0 * hw32, i0 = r0 / wo32, j0 = r0 - i0 * wo32;
+    // output pixel of input pixel (i, j) and tap (a, b): (2i + a, 2j + b) of a 2h x 2w image;
+    // relative to output row 2 i0 of image img0, input row offset R from row i0 (across
+    // image boundaries too: 2h output rows per h input rows)
+    const long obase = ((long)img0 * 2 * p.ho + 2 * i0) * 2 * p.wo;
+    const __amdgpu_buffer_rsrc_t os = dma::brsrc((const bf16*)p.out + obase * p.out_ld + p.out_off);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const unsigned d = wm * TM + i * 16 + frow;
+      const bool ok = m0 + d < (unsigned)p.M;
+      const unsigned pos = j0 + d;
+      int R = (int)((float)pos * invw);
+      int col = (int)pos - R * (int)wo32;
+      if (col >= (int)wo32) { ++R; col -= (int)wo32; }
+      if (col < 0) { --R; col += (int)wo32; }
+#pragma unroll
+      for (int q = 0; q < FP; ++q) {
+        const int cl = wn * TN + 32 * q + 8 * g;
+        const float4 b0 = *reinterpret_cast<const float4*>(bias_s + cl);
+        const float4 b1 = *reinterpret_cast<const float4*>(bias_s + cl + 4);
+        const float bj[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        bf16x8 o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float v = acc[i][2 * q + (k >> 2)][k & 3] + bj[k];
+          if (relu) v = fmaxf(v, 0.f);
+          const float vs = ok ? v : 0.f;
+          s1[q][k] += vs;
+          s2v[q][k] = fmaf(vs, vs, s2v[q][k]);
+          o[k] = (bf16)v;
+        }
+        const unsigned opx = (unsigned)((2 * R + (tq[q] >> 1)) * 2 * p.wo + 2 * col + (tq[q] & 1));
+        const unsigned off = (unsigned)(opx * out_px + cq[q] * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, o), os, ok ? off : dma::OOB, 0, 0);
+      }
+    }
+  };
+
+  if (S > 0) {
+    set_issue(0);
+    issue(0);
+    advance();
+  }
+  int ck = 0, cj = 0;
+  bool stored = false;
+  for (int t = 0; t < S; ++t) {
+    if (stored) dma::wait_vm<NS>(); else dma::wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < S) {
+      issue((t + 1) & 1);
+      advance();
+    }
+    compute(t & 1);
+    stored = false;
+    if (++ck == nk) {
+      epilogue(cj);
+      zero();
+      ck = 0;
+      ++cj;
+      stored = true;
+    }
+  }
+  if (stats) {  // fold the 16 pixel lanes, one row per (XCD, slot / nblocks, wave row)
+    const long row = ((long)xcd * gs + s2) * WM + wm;
+    float* st = p.stats + row * 2 * p.N;
+#pragma unroll
+    for (int q = 0; q < FP; ++q)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float a1 = s1[q][k], a2 = s2v[q][k];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a1 += __shfl_xor(a1, o, 64);
+          a2 += __shfl_xor(a2, o, 64);
+        }
+        if (frow == 0) {
+          const int n = n0 + wn * TN + 32 * q + 8 * g + k;
+          st[n] = a1;
+          st[p.N + n] = a2;
+        }
+      }
+  }
+}
+
 // ----------------------------------------------------------------------------
 namespace {
 struct Cfg2 {
@@ -531,6 +733,32 @@ bool fwd2_pers(const FwdArgs& a, bool bf16) {
   return en && fwd2_t256(a, bf16) && !a.scatter && !a.border && !a.bias && !a.flags &&
          a.hs == 2 * a.ho && a.ws == 2 * a.wo && a.cin % 64 == 0 && a.dyc == 0xa5 && a.dxc == 0x99 && !a.cin1 && a.M < (1L << 31) &&
          (2L * (256 / a.wo + 2) + 2) * a.ws * a.a_ld * 2 < (1L << 31);  // (a tile's source span: 32-bit offsets)
+}
+
+static int cu_count();
+// the Conv2DTranspose forward in training (bias or folded per-column bias, ReLU, BN partial
+// sums; no affine) on
+// tconv_fwd2p_kernel; CNNITMO_TFWD2P=0: tconv_ws / tconv_stream
+bool tfwd2p_handles(const FwdArgs& a, bool bf16) {
+  static const int en = [] {
+    const char* e = getenv("CNNITMO_TFWD2P");
+    return e ? atoi(e) : 1;
+  }();
+  const int gx = std::max(cu_count() / 8, 1);
+  return en && bf16 && a.scatter && a.ntaps == 1 && a.N % 256 == 0 && a.cin % 64 == 0 && a.cout % 8 == 0 &&
+         !a.border && !(a.flags & ~(CNNITMO_RELU | CNNITMO_STATS | CNNITMO_BIAS_PER_COL)) && a.M < (1L << 31) && a.a_off % 8 == 0 &&
+         a.a_ld % 8 == 0 && a.out_ld % 8 == 0 && a.out_off % 8 == 0 && gx % (a.N / 256) == 0 &&
+         (long)256 * a.a_ld * 2 < (1L << 31) && (2L * (256 / a.wo + 3)) * 2 * a.wo * a.out_ld * 2 < (1L << 31);
+}
+long tfwd2p_stat_rows(const FwdArgs& a) { return 8L * (std::max(cu_count() / 8, 1) / (a.N / 256)) * 2; }
+int launch_tfwd2p(FwdArgs a, hipStream_t s, const char* what) {
+  CNN_REQUIRE(tfwd2p_handles(a, true), "%s: unsupported by tconv_fwd2p", what);
+  CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
+  a.mblocks = (int)((a.M + 255) / 256);
+  a.nblocks = a.N / 256;
+  const int g = 8 * std::max(cu_count() / 8, 1);
+  hipLaunchKernelGGL((tconv_fwd2p_kernel<256, 256, 2, 4>), dim3((unsigned)g), dim3(512), 0, s, a);
+  return cnnitmo_check_launch(what);
 }
 
 static int cu_count() {
