@@ -528,7 +528,7 @@ extern "C" const char* cnnitmo_tconv2x2_kernel_name(int dtype, int n, int h, int
     return tconv_stream_name(dgrad ? 1 : 0, h, w, cin, cout, false);
   if (!dgrad && dtype == CNNITMO_BF16 &&
       tfwd2p_handles(tconv_fwd_args(n, h, w, cin, cout, CNNITMO_RELU | CNNITMO_STATS), true))
-    return "tconv_fwd2p_kernel<bf16,256x256>";  // (the training forward; inference: tconv_ws)
+    return "tconv_fwd2p_kernel<bf16,256x256>";
   if (dtype == CNNITMO_BF16 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout))
     return tconv_ws_name(dgrad ? 1 : 0, cin, cout);
   if (dtype == CNNITMO_F32 && tconv_ws_handles(dgrad ? 1 : 0, cin, cout, true))

@@ -474,8 +474,8 @@ __global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs
   constexpr int NA = C::NA, NB = C::NB, STAGE = C::STAGE, FP = FN / 2;
   constexpr int NS = FM * FP;  // epilogue stores per wave per tile
   static_assert(FN % 2 == 0 && TN % 32 == 0, "column pairs");
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + BN * 4];
-  float* bias_s = reinterpret_cast<float*>(smem + 2 * STAGE);
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE + 3 * BN * 4];
+  float* bias_s = reinterpret_cast<float*>(smem + 2 * STAGE);  // [3][BN]: bias, affine scale, shift
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -492,10 +492,12 @@ __global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs
   const bf16* __restrict__ A = (const bf16*)p.a;
   const bf16* __restrict__ B = (const bf16*)p.b;
   const unsigned hw32 = (unsigned)((long)p.ho * p.wo), wo32 = (unsigned)p.wo;
-  const bool relu = p.flags & CNNITMO_RELU, stats = p.flags & CNNITMO_STATS;
+  const bool relu = p.flags & CNNITMO_RELU, stats = p.flags & CNNITMO_STATS, aff = p.flags & CNNITMO_AFFINE;
   for (int i = tid; i < BN; i += WM * WN * 64) {
-    const int n = n0 + i;
-    bias_s[i] = !p.bias ? 0.f : p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : n - (n / p.cout) * p.cout];
+    const int n = n0 + i, co = n - (n / p.cout) * p.cout;
+    bias_s[i] = !p.bias ? 0.f : p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : co];
+    bias_s[BN + i] = aff ? p.aff_scale[co] : 1.f;
+    bias_s[2 * BN + i] = aff ? p.aff_shift[co] : 0.f;
   }
   // the lane's two 8-column groups: tap and channel (8 | cout: a group never straddles taps)
   int tq[FP], cq[FP];
@@ -512,12 +514,12 @@ __global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs
 #pragma unroll
   for (int i = 0; i < NB; ++i)
     vob[i] = (unsigned)(((long)pair_perm((wave * NB + i) * 8 + sub) * K + ((i & 1) ? cA1 : cA0) * VE) * 2);
-  const dma::i32x4 rb = dma::rsrc((uintptr_t)(B + (size_t)n0 * K));
-  dma::i32x4 ra;
+  dma::i32x4 ra, rb;
   int i_k = 0, i_j = 0;
   auto set_issue = [&](int j) {
     const unsigned m0 = (unsigned)(mbeg + s2 + j * gs) * BM;
     ra = dma::rsrc((uintptr_t)(A + (size_t)m0 * p.a_ld + p.a_off));
+    rb = dma::rsrc((uintptr_t)(B + (size_t)n0 * K));
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       const unsigned d = (wave * NA + i) * 8 + sub;
@@ -594,11 +596,21 @@ __global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs
         const float4 b0 = *reinterpret_cast<const float4*>(bias_s + cl);
         const float4 b1 = *reinterpret_cast<const float4*>(bias_s + cl + 4);
         const float bj[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        float sj[8], hj[8];
+        if (aff) {
+          const float4 c0 = *reinterpret_cast<const float4*>(bias_s + BN + cl);
+          const float4 c1 = *reinterpret_cast<const float4*>(bias_s + BN + cl + 4);
+          const float4 d0 = *reinterpret_cast<const float4*>(bias_s + 2 * BN + cl);
+          const float4 d1 = *reinterpret_cast<const float4*>(bias_s + 2 * BN + cl + 4);
+          sj[0] = c0.x; sj[1] = c0.y; sj[2] = c0.z; sj[3] = c0.w; sj[4] = c1.x; sj[5] = c1.y; sj[6] = c1.z; sj[7] = c1.w;
+          hj[0] = d0.x; hj[1] = d0.y; hj[2] = d0.z; hj[3] = d0.w; hj[4] = d1.x; hj[5] = d1.y; hj[6] = d1.z; hj[7] = d1.w;
+        }
         bf16x8 o;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           float v = acc[i][2 * q + (k >> 2)][k & 3] + bj[k];
           if (relu) v = fmaxf(v, 0.f);
+          if (aff) v = fmaf(v, sj[k], hj[k]);
           const float vs = ok ? v : 0.f;
           s1[q][k] += vs;
           s2v[q][k] = fmaf(vs, vs, s2v[q][k]);
@@ -611,8 +623,8 @@ __global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs
     }
   };
 
+  set_issue(0);  // (a workgroup without tiles computes addresses it never uses)
   if (S > 0) {
-    set_issue(0);
     issue(0);
     advance();
   }
@@ -736,8 +748,8 @@ bool fwd2_pers(const FwdArgs& a, bool bf16) {
 }
 
 static int cu_count();
-// the Conv2DTranspose forward in training (bias or folded per-column bias, ReLU, BN partial
-// sums; no affine) on
+// the bf16 Conv2DTranspose forward (bias or folded per-column bias, ReLU, inference affine,
+// BN partial sums; the plan depends on the sizes only, so the stat-row query matches) on
 // tconv_fwd2p_kernel; CNNITMO_TFWD2P=0: tconv_ws / tconv_stream
 bool tfwd2p_handles(const FwdArgs& a, bool bf16) {
   static const int en = [] {
@@ -746,7 +758,7 @@ bool tfwd2p_handles(const FwdArgs& a, bool bf16) {
   }();
   const int gx = std::max(cu_count() / 8, 1);
   return en && bf16 && a.scatter && a.ntaps == 1 && a.N % 256 == 0 && a.cin % 64 == 0 && a.cout % 8 == 0 &&
-         !a.border && !(a.flags & ~(CNNITMO_RELU | CNNITMO_STATS | CNNITMO_BIAS_PER_COL)) && a.M < (1L << 31) && a.a_off % 8 == 0 &&
+         !a.border && !(a.flags & ~(CNNITMO_RELU | CNNITMO_STATS | CNNITMO_BIAS_PER_COL | CNNITMO_AFFINE)) && a.M < (1L << 31) && a.a_off % 8 == 0 &&
          a.a_ld % 8 == 0 && a.out_ld % 8 == 0 && a.out_off % 8 == 0 && gx % (a.N / 256) == 0 &&
          (long)256 * a.a_ld * 2 < (1L << 31) && (2L * (256 / a.wo + 3)) * 2 * a.wo * a.out_ld * 2 < (1L << 31);
 }

@@ -189,6 +189,33 @@ def test_tconv(dt, cin, cout, H, W):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("cin,cout,H,W", [(512, 256, 5, 7), (256, 128, 9, 40)])
+def test_tconv_affine_inference_epilogue(dt, cin, cout, H, W):
+    """Conv2DTranspose forward with the inference BN affine after the ReLU (no sums): bf16 runs
+    tconv_fwd2p_kernel, whose plan depends on the sizes only (the stat-row query matches
+    whatever flags the launch carries)."""
+    from cnn_itmo_amd import ops
+    rng = np.random.default_rng(cin + 1)
+    N = 2
+    x = rng.standard_normal((N, H, W, cin)).astype(np.float32)
+    k = (rng.standard_normal((2, 2, cout, cin)) * 0.1).astype(np.float32)
+    b = rng.standard_normal(cout).astype(np.float32)
+    sc = rng.uniform(-2, 2, cout).astype(np.float32)
+    sh = rng.standard_normal(cout).astype(np.float32)
+    d = DT[dt]
+    ref = np.maximum(R.tconv2x2s2(rnd(x, dt), rnd(k, dt), b), 0) * sc + sh
+    kf = torch.empty(k.size, dtype=TDT[dt], device="cuda")
+    kT = torch.empty(k.size, dtype=TDT[dt], device="cuda")
+    ops.prep_tconv(d, torch.tensor(k).cuda(), cout, cin, kf, kT)
+    out = torch.zeros(N * 2 * H * 2 * W * cout, dtype=TDT[dt], device="cuda")
+    ops.tconv_fwd(d, ops.View(dev(x, dt).reshape(-1), N, H, W, cin, cin), kf, torch.tensor(b).cuda(),
+                  ops.View(out, N, 2 * H, 2 * W, cout, cout, 0), flags=1 | 4,
+                  aff=(torch.tensor(sc).cuda(), torch.tensor(sh).cuda()))
+    torch.cuda.synchronize()
+    close(host(out).reshape(ref.shape), ref, dt, "tconv affine")
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
 def test_im2col_columns_exact(dt):
     """cnnitmo_im2col_c3 == the (r, s, c)-ordered 3x3x3 patches (+5 zero columns), bit-exact,
     over several 256-pixel row segments (the last one partial) and zero-padded rows >= Hv."""
