@@ -375,6 +375,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // the tile's last item, so that item's MFMAs cover their HBM latency; otherwise after the
   // MFMAs (the BN-64 kernels sit at 256 VGPRs).  Early vs late on the 32-column kernels:
   // 215.4 / 215.4 vs 215.4 / 213.9 frames/s (profiles/r05/r05d_ab_early_r.txt).
+  // (An L2 touch of the r lines at the start of the tile's last item, one 4-byte LDS-DMA
+  // per lane: 1-11 % slower on every 64-column fused dgrad, profiles/r05/r05z3_ab_r_touch.txt.)
   // (Single-buffered fragments on the 64-column kernels, which frees the registers for early
   // r loads: every 64-column fused dgrad 8-27 % slower, 218.0 -> 212.2 frames/s,
   // profiles/r05/r05q_ab_sb64_early_r.txt.)
