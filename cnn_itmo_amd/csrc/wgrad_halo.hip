@@ -56,6 +56,7 @@ struct WHArgs {
   long slab;
   int strips, cbm, cbn, rsplits;
   long rows_per;  // row steps per workgroup
+  int cbase;      // first input channel of the launch's column blocks (a split 128 + 64 launch)
 };
 
 // Waves: three groups (one per kernel row r = 0, 1, 2), each WM x WN over the
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
   bid /= p.cbm * p.cbn;
   const int strip = bid % p.strips;
   const int rs = bid / p.strips;
-  const int m0 = (cb / p.cbn) * BM, n0 = (cb % p.cbn) * BN;
+  const int m0 = (cb / p.cbn) * BM, n0 = p.cbase + (cb % p.cbn) * BN;
   const int x0 = strip * TW;
   const long total_rows = (long)p.nimg * p.H;
   const long g0 = (long)rs * p.rows_per;
@@ -367,7 +368,7 @@ __global__ __launch_bounds__(3 * (BM / 32) * wf_wn(BN) * 64) void wgrad_halo_f32
   bid /= p.cbm * p.cbn;
   const int strip = bid % p.strips;
   const int rs = bid / p.strips;
-  const int m0 = (cb / p.cbn) * BM, n0 = (cb % p.cbn) * BN;
+  const int m0 = (cb / p.cbn) * BM, n0 = p.cbase + (cb % p.cbn) * BN;
   const int x0 = strip * TW;
   const long total_rows = (long)p.nimg * p.H;
   const long g0 = (long)rs * p.rows_per;
@@ -601,6 +602,7 @@ int wh_occupancy(int bm, int bn, int tw) {
 struct WHPlan {
   int bm, bn, tw, strips, cbm, cbn, rsplits, smem;
   long rows_per;
+  bool split;  // cin 192: a 128-column launch and a 64-column launch instead of two 96-column blocks
 };
 
 bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = false) {
@@ -616,6 +618,12 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
   }();
   pl.bn = cin % 96 == 0 ? 96 : (cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0));
   if (!cat && cout % 64 == 0 && cin % 128 == 0 && (bn128 >= 2 || (bn128 == 1 && pl.bn != 96))) pl.bn = 128;
+  static const int split192 = [] {
+    const char* e = getenv("CNNITMO_WH_SPLIT192");
+    return e ? atoi(e) : 1;
+  }();
+  pl.split = !cat && split192 && cin == 192 && cout % 64 == 0;
+  if (pl.split) pl.bn = 128;  // (the planner below sizes the 128-column launch; the 64 one follows it)
   if (!pl.bm || !pl.bn) return false;
   // 128-column strips also when w % 128 != 0 (a partial last strip): enc2a at 960
   // columns 1.12 -> 0.99 ms (tools/ab_env.sh); CNNITMO_WH_TW128=0 restores 64
@@ -626,7 +634,7 @@ bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = fals
   pl.tw = (pl.bm * pl.bn <= 32 * 64 && (w % 128 == 0 || (tw128 && w % 64 == 0))) ? 128 : 64;
   pl.strips = (w + pl.tw - 1) / pl.tw;  // a partial last strip reads zero columns
   pl.cbm = cout / pl.bm;
-  pl.cbn = cin / pl.bn;
+  pl.cbn = pl.split ? 1 : cin / pl.bn;
   const long rows = (long)n * h;
   const long per = (long)pl.strips * pl.cbm * pl.cbn;
   // whole rounds of resident workgroups: slots = CUs x workgroups per CU (LDS- or
@@ -746,6 +754,12 @@ int launch_wgrad_halo(const bf16* x, long x_ld, int x_off, const bf16* dz, int n
   a.out = ws; a.slab = (long)cout * 9 * cin;
   a.strips = pl.strips; a.cbm = pl.cbm; a.cbn = pl.cbn; a.rsplits = pl.rsplits; a.rows_per = pl.rows_per;
   const unsigned grid = (unsigned)(pl.strips * pl.cbm * pl.cbn * pl.rsplits);
+  if (pl.split) {  // channels [0, 128) on 64 x 128 blocks, [128, 192) on 64 x 64 blocks; the same slabs
+    wh_launch<64, 128, 64>(a, grid, s);
+    a.cbase = 128;
+    wh_launch<64, 64, 64>(a, grid, s);
+    return pl.strips * pl.rsplits;
+  }
   if (cat) {
     if (pl.bm == 64) wh_launch<64, 96, 64, true>(a, grid, s);
     else wh_launch<32, 96, 64, true>(a, grid, s);
@@ -764,7 +778,10 @@ const char* wgrad_halo_name(int n, int h, int w, int cin, int cout, bool cat) {
   WHPlan pl;
   if (!wh_plan(n, h, w, cin, cout, pl, cat)) return "";
   static thread_local char buf[64];
-  snprintf(buf, sizeof(buf), "wgrad_halo_kernel<%d,%d,%d%s>", pl.bm, pl.bn, pl.tw, cat ? ",cat" : "");
+  if (pl.split)
+    snprintf(buf, sizeof(buf), "wgrad_halo_kernel<%d,128+64,%d>", pl.bm, pl.tw);
+  else
+    snprintf(buf, sizeof(buf), "wgrad_halo_kernel<%d,%d,%d%s>", pl.bm, pl.bn, pl.tw, cat ? ",cat" : "");
   return buf;
 }
 
