@@ -375,6 +375,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   // the tile's last item, so that item's MFMAs cover their HBM latency; otherwise after the
   // MFMAs (the BN-64 kernels sit at 256 VGPRs).  Early vs late on the 32-column kernels:
   // 215.4 / 215.4 vs 215.4 / 213.9 frames/s (profiles/r05/r05d_ab_early_r.txt).
+  // (r through the free ring stage by LDS-DMA during the tile's last item, the next tile's
+  // first item loaded after the MFMAs, the epilogue reading r from LDS: 15-28 % slower on
+  // every 64-column fused dgrad with streamed weights, profiles/r05/r05z10_ab_r_via_lds.txt;
+  // without any epilogue these launches run 19-57 % faster, r05z8_probe_noepi2.txt.)
   // (An L2 touch of the r lines at the start of the tile's last item, one 4-byte LDS-DMA
   // per lane: 1-11 % slower on every 64-column fused dgrad, profiles/r05/r05z3_ab_r_touch.txt.)
   // (Single-buffered fragments on the 64-column kernels, which frees the registers for early
@@ -827,7 +831,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       issued += L;
       mq[ST - 1] = issued;
     }
-    if (ep.ch == nch - 1 && HALO_PROBE_NOEPI && EPI == 1) {  // (probe: the accumulators stay live)
+#ifndef HALO_PROBE_NOEPI2
+#define HALO_PROBE_NOEPI2 0
+#endif
+    if (ep.ch == nch - 1 && ((HALO_PROBE_NOEPI && EPI == 1) || (HALO_PROBE_NOEPI2 && EPI == 2))) {  // (probe: the accumulators stay live)
       float z = 0.f;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
