@@ -653,10 +653,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       for (int f = 0; f < FM; ++f) {
         const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
         const bool ok = oh0 + rr < p.ho && e.x0 + col < p.wo;
-        const long m = m0 + (long)rr * p.wo + col;
-        float v[8], gr[8];
+        float gr[8];
         routed(f, q, gr);
         const bf16x8 rq = __builtin_bit_cast(bf16x8, rv[f][q]);
+        bf16x8 o;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           // (as cnnitmo_bn_bwd_apply_pooled: the bf16 gradient, then the routed pooled one)
@@ -664,17 +664,19 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           if constexpr (POOL) gk += gr[k];
           const float r = to_f32(rq[k]);
           if (fz) {
-            v[k] = to_f32(from_f32<bf16>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f));
-            sa[q][k] += (ok && rr == 0) ? v[k] : 0.f;
-            sb[q][k] += (ok && rr == 1) ? v[k] : 0.f;
+            // (an out-of-image pixel reads r = 0, so its dz is 0 and adds nothing to the sums)
+            o[k] = from_f32<bf16>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f);
+            if (rr == 0) sa[q][k] += to_f32(o[k]);
+            else sb[q][k] += to_f32(o[k]);
           } else {
-            v[k] = gk;
+            o[k] = from_f32<bf16>(gk);
           }
         }
+        const long m = m0 + (long)rr * p.wo + col;
         uint4* dst = !ok ? h_sink + lane
                      : fz ? reinterpret_cast<uint4*>(Z + (size_t)m * cbn + (c - c0))
                           : reinterpret_cast<uint4*>(O + (size_t)m * p.out_ld + p.out_off + c);
-        *dst = __builtin_bit_cast(uint4, pack8(v));
+        *dst = __builtin_bit_cast(uint4, o);
       }
     }
     zero_acc();
