@@ -174,3 +174,23 @@ def test_fused_head_size_fallback():
     assert not BlockStage._head_fits(st, 32)
     st = SimpleNamespace(eng=SimpleNamespace(h_valid=1080), vout=SimpleNamespace(w=1920))
     assert BlockStage._head_fits(st, 86) and not BlockStage._head_fits(st, 87)
+
+
+def test_tconv_planner_choices(lib):
+    """The Conv2DTranspose planners (host logic, no GPU work): up6-up8 run the persistent
+    kernels in bf16 with one BN partial-sum row per (XCD, slot / column blocks, wave row), up9 the
+    streamed kernels; the row count depends only on the sizes, so the engine's query matches the
+    launch whatever epilogue flags it carries."""
+    import ctypes
+    rows = lib.cnnitmo_tconv2x2_stat_rows
+    rows.restype = ctypes.c_long
+    name = lib.cnnitmo_tconv2x2_kernel_name
+    name.restype = ctypes.c_char_p
+    cus = 256  # (no device here: the planners assume MI355X's 256 CUs)
+    for (h, w, cin, cout) in [(272, 480, 256, 128), (136, 240, 512, 256), (68, 120, 512, 512)]:
+        nblocks = 4 * cout // 256
+        assert rows(1, 32, h, w, cin, cout) == 8 * (cus // 8 // nblocks) * 2
+        assert name(1, 32, h, w, cin, cout, 0) == b"tconv_fwd2p_kernel<bf16,256x256>"
+        assert name(1, 32, h, w, cin, cout, 1) == b"igemm_fwd2p_kernel<bf16,256x256>"
+    assert name(1, 32, 544, 960, 128, 64, 0).startswith(b"tconv_stream_kernel")
+    assert name(0, 8, 272, 480, 256, 128, 0).startswith(b"tconv_ws_kernel<f32")  # fp32: unchanged
