@@ -300,8 +300,10 @@ def cpu_baseline(args, P_init, H, W, train=True):
     net = R.UNetRef(P_init, np.float32)
     cores, blas, model = _host_info()
     # the oracle runs its convs' row bands on R._POOL threads, each in BLAS: split the CPU share
-    # between them so that the threads in use never exceed it
-    per = max(1, blas // R._POOL)
+    # between them so that the threads in use (band threads x BLAS threads) never exceed it
+    pool0 = R._POOL
+    R._POOL = bands = max(1, min(pool0, blas))
+    per = max(1, blas // bands)
     from threadpoolctl import threadpool_limits
     with threadpool_limits(limits=per, user_api="blas"):
         k, t0 = 0, time.perf_counter()
@@ -313,13 +315,14 @@ def cpu_baseline(args, P_init, H, W, train=True):
             if time.perf_counter() - t0 >= 10.0:
                 break
         dt = (time.perf_counter() - t0) / k
+    R._POOL = pool0
     frac = (h * w) / float(H * W)
     what = "train step (fwd+bwd)" if train else "inference forward (BN moving stats)"
     return {"value": frac / dt, "unit": "1080p frames/s (%s, fp32)" % ("fwd+bwd" if train else "fwd"),
-            "cores": R._POOL * per, "kind": "port",
+            "cores": bands * per, "kind": "port",
             "sample": f"oracle/unet_ref.py numpy fp32 {what} on 1 frame {w}x{h} "
                       f"({frac:.4f} of a 1920x{H} frame, scaled by pixel count), {k} x {dt:.2f} s",
-            "seconds": dt, "padded_h": H, "affinity_cores": cores, "blas_threads": per, "band_threads": R._POOL,
+            "seconds": dt, "padded_h": H, "affinity_cores": cores, "blas_threads": per, "band_threads": bands,
             "cpu_model": model, "threads_note": THREADS_NOTE}
 
 

@@ -34,6 +34,7 @@ sz = C.c_size_t
 # name -> (restype, argtypes).  Mirrors include/cnn_itmo.h exactly.
 SIGNATURES = {
     "cnnitmo_version": (i32, []),
+    "cnnitmo_consumer_rows": (i32, []),
     "cnnitmo_last_error": (C.c_char_p, []),
     "cnnitmo_augment_affine": (i32, [i32, vp, i32, i32, i32, i32, vp, vp, f32, vp, vp]),
     "cnnitmo_tonemap_workspace_bytes": (sz, [i32]),
@@ -139,6 +140,9 @@ def load(path: str | None = None):
         fn = getattr(lib, name)  # AttributeError if the export is missing
         fn.restype = res
         fn.argtypes = args
+    if lib.cnnitmo_consumer_rows() != CONSUMER_ROWS:  # a compile-time sizing constant of the ABI
+        raise CnnItmoError(f"{p}: built with {lib.cnnitmo_consumer_rows()} consumer-sum rows, "
+                           f"the binding sizes {CONSUMER_ROWS} (cnnitmo_version {lib.cnnitmo_version()})")
     if path is None:
         _lib = lib
     return lib

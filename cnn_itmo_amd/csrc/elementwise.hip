@@ -31,7 +31,10 @@ int cnnitmo_check_launch(const char* what) {
   return CNNITMO_OK;
 }
 extern "C" const char* cnnitmo_last_error(void) { return g_err; }
-extern "C" int cnnitmo_version(void) { return 1; }
+// 2: CNNITMO_CONSUMER_ROWS 16 -> 64 (query it with cnnitmo_consumer_rows) and cnnitmo_bn_apply's
+//    scale / shift must be 16-byte aligned
+extern "C" int cnnitmo_version(void) { return 2; }
+extern "C" int cnnitmo_consumer_rows(void) { return CNNITMO_CONSUMER_ROWS; }
 
 static inline int grid_for(long work, int per_block = 256, int cap = 8192) {
   long b = (work + per_block - 1) / per_block;

@@ -749,8 +749,12 @@ bool fwd2_pers(const FwdArgs& a, bool bf16) {
 
 static int cu_count();
 // the bf16 Conv2DTranspose forward (bias or folded per-column bias, ReLU, inference affine,
-// BN partial sums; the plan depends on the sizes only, so the stat-row query matches) on
-// tconv_fwd2p_kernel; CNNITMO_TFWD2P=0: tconv_ws / tconv_stream
+// BN partial sums) on tconv_fwd2p_kernel; CNNITMO_TFWD2P=0: tconv_ws / tconv_stream.  The plan
+// (tfwd2p_handles) depends on the sizes and flags only, so cnnitmo_tconv2x2_stat_rows (which asks
+// it with dense views) always sizes the stats buffer for the kernel the launch will run; the view
+// conditions (16-byte alignment, 32-bit buffer offsets of the strides) are not part of the plan
+// but requirements of the launch: a view that fails them is an error, never a silent fall-back to
+// a kernel with a different stat-row count.
 bool tfwd2p_handles(const FwdArgs& a, bool bf16) {
   static const int en = [] {
     const char* e = getenv("CNNITMO_TFWD2P");
@@ -758,13 +762,16 @@ bool tfwd2p_handles(const FwdArgs& a, bool bf16) {
   }();
   const int gx = std::max(cu_count() / 8, 1);
   return en && bf16 && a.scatter && a.ntaps == 1 && a.N % 256 == 0 && a.cin % 64 == 0 && a.cout % 8 == 0 &&
-         !a.border && !(a.flags & ~(CNNITMO_RELU | CNNITMO_STATS | CNNITMO_BIAS_PER_COL | CNNITMO_AFFINE)) && a.M < (1L << 31) && a.a_off % 8 == 0 &&
-         a.a_ld % 8 == 0 && a.out_ld % 8 == 0 && a.out_off % 8 == 0 && gx % (a.N / 256) == 0 &&
-         (long)256 * a.a_ld * 2 < (1L << 31) && (2L * (256 / a.wo + 3)) * 2 * a.wo * a.out_ld * 2 < (1L << 31);
+         !a.border && !(a.flags & ~(CNNITMO_RELU | CNNITMO_STATS | CNNITMO_BIAS_PER_COL | CNNITMO_AFFINE)) &&
+         a.M < (1L << 31) && gx % (a.N / 256) == 0;
 }
 long tfwd2p_stat_rows(const FwdArgs& a) { return 8L * (std::max(cu_count() / 8, 1) / (a.N / 256)) * 2; }
 int launch_tfwd2p(FwdArgs a, hipStream_t s, const char* what) {
   CNN_REQUIRE(tfwd2p_handles(a, true), "%s: unsupported by tconv_fwd2p", what);
+  CNN_REQUIRE(a.a_off % 8 == 0 && a.a_ld % 8 == 0 && a.out_ld % 8 == 0 && a.out_off % 8 == 0,
+              "%s: views must be 16-byte aligned", what);
+  CNN_REQUIRE((long)256 * a.a_ld * 2 < (1L << 31) && (2L * (256 / a.wo + 3)) * 2 * a.wo * a.out_ld * 2 < (1L << 31),
+              "%s: row strides exceed the kernel's 32-bit buffer offsets", what);
   CNN_REQUIRE(!(a.flags & CNNITMO_STATS) || a.stats, "%s: STATS without buffer", what);
   a.mblocks = (int)((a.M + 255) / 256);
   a.nblocks = a.N / 256;

@@ -942,7 +942,7 @@ class Engine:
         [conv1 32 | up9 64] (model.py:261) puts 64 + 128 B of each 192-B row in lines
         shared with the neighbouring pixels, so the pool, its BN-sum pass and enc1b's
         BN-backward apply read conv1 in half lines and up9 writes them.  Its consumer
-        (conv9, a 3x3 conv, model.py:261) then reads both members directly: cnnitmo_conv3x3_fwd_cat /
+        (conv9, a 3x3 conv, model.py:262) then reads both members directly: cnnitmo_conv3x3_fwd_cat /
         cnnitmo_conv_wgrad_cat (bf16 halo kernels; its input gradient is already split
         per member).  CNNITMO_SPLIT_CAT=0, or sizes either entry point rejects: one
         concat buffer."""
@@ -1000,7 +1000,7 @@ class Engine:
 
     def _plan_head_fusion(self):
         """The sigmoid head (model.py:276) into the inference epilogue of the 3x3 ConvBN that
-        feeds it (conv9, model.py:261): predict() then never stores that conv's 64-channel
+        feeds it (conv9, model.py:262): predict() then never stores that conv's 64-channel
         output (fp32 b8 at 1080p: 4.3 GB written and read back).  Needs: a 'c3' producer with
         BN and no Dropout / pooling / concat, consumed by the head alone, 64 channels, the halo
         kernel for its sizes.  CNNITMO_HEAD_FUSE=0: the stand-alone head kernel."""

@@ -55,6 +55,9 @@ extern "C" {
 #define CNNITMO_NO_BN 2   /* bwd: plain ReLU gradient, no BN (config-1 net)  */
 #define CNNITMO_PARITY 4  /* bwd apply: bias partials split by (h&1, w&1) -> [4][c] */
 
+/* ABI version: 2 since CNNITMO_CONSUMER_ROWS went from 16 to 64 (a caller built against the
+ * old header under-allocates cnnitmo_bn_consumer_sums' part: check cnnitmo_consumer_rows()) and
+ * cnnitmo_bn_apply started to require 16-byte aligned scale / shift. */
 int cnnitmo_version(void);
 const char* cnnitmo_last_error(void);
 
@@ -89,7 +92,7 @@ int cnnitmo_conv3x3_fwd_pool(int dtype, const void* x, int x_ld, int x_off, int 
                              int flags, const float* aff_scale, const float* aff_shift, float* stat_part,
                              const float* border, void* pool_out, int pool_ld, unsigned char* pool_idx,
                              const float* pool_sign, void* stream);
-/* The last 3x3 ConvBN (conv9 = ConvBN(64, 3, merge9), model.py:261) with the sigmoid head
+/* The last 3x3 ConvBN (conv9 = ConvBN(64, 3, merge9), model.py:262) with the sigmoid head
  * (model.py:276, Conv2D(3, 1, activation='sigmoid')) in its epilogue, for inference
  * (predict.py:62): yhat [n][h_valid][w][3] fp32 = sigmoid(y . head_w[3][cout] + head_b), y = the
  * conv's epilogue output (flags/aff as cnnitmo_conv3x3_fwd: ReLU, BN affine), never stored.
@@ -196,7 +199,7 @@ int cnnitmo_conv_wgrad(int dtype, int ntaps, const void* x, int x_ld, int x_off,
  * the uncorrected sum dz (x) r, input of cnnitmo_bn_consumer_sums. */
 
 /* cnnitmo_conv_wgrad (ntaps 9, bf16) over concatenate([x1, x2]) read from its members
- * (see cnnitmo_conv3x3_fwd_cat): c1 == 32, cin == 96 (conv9, model.py:260-261).
+ * (see cnnitmo_conv3x3_fwd_cat): c1 == 32, cin == 96 (merge9 -> conv9, model.py:261-262).
  * workspace: cnnitmo_wgrad_cat_workspace_bytes (0 = unsupported sizes). */
 size_t cnnitmo_wgrad_cat_workspace_bytes(int n, int h, int w, int c1, int cin, int cout);
 const char* cnnitmo_wgrad_cat_kernel_name(int n, int h, int w, int c1, int cin, int cout);
@@ -332,7 +335,8 @@ int cnnitmo_bn_infer_coeffs(int c, const float* gamma, const float* beta, const 
                             const float* mvar, float eps, float* scale, float* shift,
                             void* stream);
 /* y view = r*scale + shift (optionally Dropout(0.5): element (p,c) kept iff the
- * counter hash of (seed, layer, p*c_total + c) says so, kept values x2). */
+ * counter hash of (seed, layer, p*c_total + c) says so, kept values x2).  scale and shift
+ * must be 16-byte aligned (CNNITMO_EINVAL otherwise; since cnnitmo_version() 2). */
 int cnnitmo_bn_apply(int dtype, const void* r, long p, int c, const float* scale,
                      const float* shift, void* y, int y_ld, int y_off, int flags,
                      uint64_t drop_seed, int drop_layer, void* stream);
@@ -380,6 +384,9 @@ int cnnitmo_bn_bwd_apply_g3(int dtype, const float* g3, const float* wh, const v
  * MaxPooling2D consumer's share (dyp: the pooled gradient; r: the pool input's
  * view; rows = cnnitmo_bn_bwd_rows(n*(h/2)*(w/2), c)). */
 #define CNNITMO_CONSUMER_ROWS 64
+/* The row count the library was built with (== CNNITMO_CONSUMER_ROWS of this header; 16 before
+ * cnnitmo_version() 2): size part from this at run time. */
+int cnnitmo_consumer_rows(void);
 int cnnitmo_bn_consumer_sums(int mode, const float* w, const float* raw, int cout, int cin_tot, int ci0,
                              int c, const float* db, const float* vtab, const float* mean,
                              const float* invstd, float* part, void* stream);

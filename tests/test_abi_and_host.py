@@ -34,7 +34,8 @@ def test_header_exports_and_bindings(lib):
     for s in syms:
         assert hasattr(lib, s), f"{s} declared in cnn_itmo.h but not exported"
     assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
-    assert lib.cnnitmo_version() == 1
+    assert lib.cnnitmo_version() == 2
+    assert lib.cnnitmo_consumer_rows() == _lib.CONSUMER_ROWS == 64
 
 
 def test_queries_without_gpu(lib):

@@ -1,21 +1,24 @@
-"""The training composition at the benchmarked frame size against the oracle: ONE fp32
-training step (main.py:126-132 trains Keras in fp32) of U_net(input_size=(1080, 1920, 3),
-pad=True, dtype="float32") -- the real engine's planner, fused launches, coefficient
-buffers, split skip gradients and deferred pool routes at 1088 x 1920 -- on the reference's
-12 SDR frames tiled into one real-content frame, against the fp64 oracle of the same step
-(tests/golden/train1080.npz, made by tests/golden/make_train1080.py from
-tools/train1080_oracle.py; the 89 MB of fp64 gradients are kept as norms plus 4096 fixed
-samples per large tensor, every value of the small ones).
+"""The training composition at the benchmarked frame size against the oracle: ONE training step
+of U_net(input_size=(1080, 1920, 3), pad=True) -- the real engine's planner, fused launches,
+coefficient buffers, split skip gradients and deferred pool routes at 1088 x 1920 -- on the
+reference's 12 SDR frames tiled into one real-content frame, against the fp64 oracle of the same
+step (tests/golden/train1080.npz, made by tests/golden/make_train1080.py from
+tools/train1080_oracle.py; the 89 MB of fp64 gradients are kept as norms plus 4096 fixed samples
+per large tensor, every value of the small ones).  Two dtypes:
 
-Bounds, as the 128x128 test's (test_gpu_model.py::test_unet_train_step_all_74_grads_128):
-each of the 74 gradients within rel-L2 max(1e-4, 3x numpy-fp32's own deviation from fp64)
-(estimated from the samples for tensors above 4096 entries, with 25 % slack for the
-estimate; its L2 norm within the same bound exactly); the loss within max(1e-5, 3x numpy-
-fp32's) relative; the Keras moving statistics after the step within rel-L2 max(1e-6, 3x
-numpy-fp32's).  At 1080p one frame's BN statistics are still ill-conditioned in the deep
-layers (numpy-fp32 deviates up to 0.5 from fp64 on the bottleneck's weight gradients; the
-biases before a BN have a zero exact gradient, pure rounding), so the fp32 floor, not a
-fixed number, sets the bound, exactly as at 128x128."""
+* float32 (main.py:126-132 trains Keras in fp32): each of the 74 gradients within rel-L2
+  max(1e-4, 0.1x numpy-fp32's own deviation from fp64) (sampled estimate for tensors above 4096
+  entries, 25 % slack for the estimate; its L2 norm within the same bound exactly); the loss within
+  max(1e-6, 0.1x numpy-fp32's) relative; the Keras moving statistics after the step within rel-L2
+  max(1e-6, 0.1x numpy-fp32's).  numpy-fp32 sums naively and deviates up to 0.5 from fp64 on the
+  deep gradients (one frame's BN statistics are ill-conditioned there); the GPU's fp32 kernels
+  (fp32 MFMA chains, fp64 folds of the partial sums) measure ~0.01x that floor, so 0.1x leaves 10x
+  headroom and still fails a 30x regression.
+* bfloat16 (BASELINE configs[2]'s dtype, the bench's planner: split level-0 concat, the fused
+  transposed-conv BN backward, the persistent transposed convs, the routed skip dgrads): each
+  gradient within rel-L2 max(2e-3, 3x the bf16-storage oracle's deviation from fp64) -- the bound of
+  test_gpu_model.py's 128x128 bf16 test -- and the loss within 5e-3 relative; the moving statistics
+  within max(1e-5, 3x the bf16-storage oracle's)."""
 import contextlib
 import io
 import os
@@ -37,7 +40,8 @@ def _rel(a, b):
 
 
 @pytest.mark.timeout(600)
-def test_train1080_fp32_step_vs_oracle():
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_train1080_step_vs_oracle(dtype):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import cnn_itmo_amd as C
@@ -46,7 +50,7 @@ def test_train1080_fp32_step_vs_oracle():
     P, x, t = inputs()
     C.clear_session()
     with contextlib.redirect_stdout(io.StringIO()):
-        m = C.U_net(input_size=(H, W, 3), pad=True, dtype="float32", verbose=False)
+        m = C.U_net(input_size=(H, W, 3), pad=True, dtype=dtype, verbose=False)
     m.set_named_weights(P)
     eng = m._engine()
     la = eng.train_step(torch.tensor(x, dtype=torch.float32).cuda(), torch.tensor(t, dtype=torch.float32).cuda(),
@@ -55,9 +59,12 @@ def test_train1080_fp32_step_vs_oracle():
     after = m.named_weights()
     C.clear_session()
 
-    l64, l32 = float(z["loss64"]), float(z["loss32"])
-    lbound = max(1e-5, 3 * abs(l32 - l64) / l64)
-    print(f"loss gpu {la[0]:.9f} oracle {l64:.9f} (numpy fp32 {l32:.9f}): rel {abs(la[0] - l64) / l64:.2e} "
+    f32 = dtype == "float32"
+    fl = "floor/" if f32 else "floor16/"
+    l64 = float(z["loss64"])
+    lfl = abs(float(z["loss32" if f32 else "loss16"]) - l64) / l64
+    lbound = max(1e-6, 0.1 * lfl) if f32 else 5e-3
+    print(f"{dtype} loss gpu {la[0]:.9f} oracle {l64:.9f} (floor {lfl:.2e}): rel {abs(la[0] - l64) / l64:.2e} "
           f"<= {lbound:.2e};  acc gpu {la[1]:.6f} oracle {float(z['acc64']):.6f}")
     assert abs(la[0] - l64) <= lbound * l64
 
@@ -66,8 +73,8 @@ def test_train1080_fp32_step_vs_oracle():
     assert len(names) == 74 and set(names) == set(grads)
     for k in names:
         g = grads[k].reshape(-1).astype(np.float64)
-        nref, floor = float(z["norm/g/" + k]), float(z["floor/g/" + k])
-        bound = max(1e-4, 3 * floor)
+        nref, floor = float(z["norm/g/" + k]), float(z[fl + "g/" + k])
+        bound = max(1e-4, 0.1 * floor) if f32 else max(2e-3, 3 * floor)
         v = z["val/g/" + k]
         if ("idx/g/" + k) in z.files:  # sampled: ||e||^2 ~ N/S * sum over the samples
             idx = z["idx/g/" + k]
@@ -78,13 +85,14 @@ def test_train1080_fp32_step_vs_oracle():
             ok = err <= bound
         nerr = abs(float(np.linalg.norm(g)) - nref) / max(nref, 1e-300)
         ok = ok and nerr <= bound
-        print(f"{k:40s} rel-L2 {err:.2e}  |norm| {nerr:.2e}  floor {floor:.2e}  ratio {err / max(floor, 1e-12):.2f}")
+        print(f"{dtype} {k:40s} rel-L2 {err:.2e}  |norm| {nerr:.2e}  floor {floor:.2e}  "
+              f"ratio {err / max(floor, 1e-12):.3f}")
         if not ok:
             bad[k] = (err, nerr, floor)
     for k in sorted(n[6:] for n in z.files if n.startswith("val/m/")):
-        floor = float(z["floor/m/" + k])
+        floor = float(z[fl + "m/" + k])
         err = _rel(np.asarray(after[k], np.float64).reshape(-1), z["val/m/" + k])
-        print(f"{k:40s} rel-L2 {err:.2e}  floor {floor:.2e}")
-        if err > max(1e-6, 3 * floor):
+        print(f"{dtype} {k:40s} rel-L2 {err:.2e}  floor {floor:.2e}")
+        if err > (max(1e-6, 0.1 * floor) if f32 else max(1e-5, 3 * floor)):
             bad[k] = (err, floor)
     assert not bad, bad

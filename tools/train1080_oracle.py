@@ -1,8 +1,13 @@
-"""The fp64 (and fp32) numpy oracle of ONE training step at the benchmarked frame size
-(test infrastructure: tests/test_gpu_train1080.py runs it in a subprocess beside the GPU
-suite and compares the GPU step with it).
+"""The fp64 (and fp32, and bf16-storage) numpy oracle of ONE training step at the benchmarked
+frame size (test infrastructure, CPU only: tests/golden/make_train1080.py reduces its outputs to
+the committed fixture tests/golden/train1080.npz, which tests/test_gpu_train1080.py reads; the
+GPU tests never run this script).
 
-    python tools/train1080_oracle.py --out /tmp/o.npz [--dtype float64|float32]
+    python tools/train1080_oracle.py --out /tmp/o.npz [--dtype float64|float32|bf16store]
+
+bf16store: fp64 arithmetic with every stored tensor rounded to bfloat16 (UNetRef(store=
+R.round_bf16), the emulation test_gpu_model.py's 128x128 bf16 test uses): the noise floor a
+bf16-storage implementation with wide accumulation is held to.
 
 Input: the 12 reference SDR frames tiled into one real-content 1080x1920 frame
 (tests/golden/make_golden.mosaic1080), zero-padded to 1088 rows as U_net(pad=True) pads
@@ -48,11 +53,11 @@ def inputs():
     return P, x, t
 
 
-def run(dtype, out):
+def run(dtype, out, store=None):
     P, x, t = inputs()
     xp = np.zeros((1, HP, W, 3))
     xp[:, :H] = x
-    net = R.UNetRef(P, dtype)
+    net = R.UNetRef(P, dtype, store=store)
     t0 = time.perf_counter()
     net.forward(xp.astype(dtype), training=True, seed=SEED)
     t1 = time.perf_counter()
@@ -71,13 +76,16 @@ def run(dtype, out):
     tmp = out + ".tmp.npz"
     np.savez(tmp, **d)
     os.replace(tmp, out)
-    print(f"[train1080_oracle] {np.dtype(dtype).name}: fwd {t1 - t0:.1f} s, bwd {t2 - t1:.1f} s, loss {loss:.9f}",
+    print(f"[train1080_oracle] {np.dtype(dtype).name}{' bf16 storage' if store else ''}: fwd {t1 - t0:.1f} s, bwd {t2 - t1:.1f} s, loss {loss:.9f}",
           file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
-    ap.add_argument("--dtype", default="float64", choices=["float64", "float32"])
+    ap.add_argument("--dtype", default="float64", choices=["float64", "float32", "bf16store"])
     a = ap.parse_args()
-    run(np.float64 if a.dtype == "float64" else np.float32, a.out)
+    if a.dtype == "bf16store":
+        run(np.float64, a.out, store=R.round_bf16)
+    else:
+        run(np.float64 if a.dtype == "float64" else np.float32, a.out)
