@@ -664,7 +664,10 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           if constexpr (POOL) gk += gr[k];
           const float r = to_f32(rq[k]);
           if (fz) {
-            // (an out-of-image pixel reads r = 0, so its dz is 0 and adds nothing to the sums)
+            // (an out-of-image pixel reads r = 0, so its dz is 0 and adds nothing to the sums: the
+            // sums take no `ok` select.  This holds because rv comes from load_r16's raw-buffer loads
+            // at r_off, which is OOB (the load returns 0) for every out-of-image or out-of-range
+            // piece; the fp32 twin, epilogue_bnb32, keeps the select.)
             o[k] = from_f32<bf16>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f);
             if (rr == 0) sa[q][k] += to_f32(o[k]);
             else sb[q][k] += to_f32(o[k]);
@@ -1005,9 +1008,11 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
 template <typename T, int BN, int EPI>
 void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
   if constexpr (EPI == 2) {
-    if (h.f.pool_out) {  // the routed pooled gradient (cnnitmo_conv3x3_dgrad_bn_pooled)
-      if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
-      else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true>), dim3(grid), dim3(NT), 0, s, h);
+    if (h.f.pool_out) {  // the routed pooled gradient (cnnitmo_conv3x3_dgrad_bn_pooled; 32-column blocks, halo_plan)
+      if constexpr (BN == 32) {
+        if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
+        else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true>), dim3(grid), dim3(NT), 0, s, h);
+      }
       return;
     }
   }

@@ -1,6 +1,10 @@
 """Issue/wait attribution of a kernel's wave cycles from tools/pmc_attrib.sh's four passes.
 
-    python tools/pmc_attrib.py gpurun_out/attrib_<tag> [kernel-label filter] [--json out.json]
+    python tools/pmc_attrib.py gpurun_out/attrib_<tag> [kernel-label filter] [--json out.json] [--steps N]
+
+--steps N: the profiled program ran N identical steps (tools/recipe.sh benchattrib): the launches
+of one label are told apart by their position in the step (label#k = the k-th launch of that
+kernel in a step), so that one kernel's layers get a row each.
 
 Per kernel label (tools/pmc_traffic.label), summed over its dispatches in each pass:
   * SQ_WAVE_CYCLES = SQ_WAIT_ANY + SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY (disjoint,
@@ -27,7 +31,7 @@ from tools.pmc_traffic import label  # noqa: E402
 SIMDS, XCDS = 256 * 4, 8
 
 
-def load(d):
+def load(d, steps=0):
     """label -> counter -> (sum over dispatches, dispatches); wall seconds per label."""
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names, wall = {}, {}
@@ -38,6 +42,15 @@ def load(d):
             names[key] = label(r["Kernel_Name"])
             if "End_Timestamp" in r:
                 wall[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    if steps:  # label#k: the k-th launch of the label within a step (per pass file)
+        byf = collections.defaultdict(list)
+        for key in names:
+            byf[(key[0], names[key])].append(key)
+        for (_, lab), keys in byf.items():
+            keys.sort(key=lambda k: k[1])
+            per_step = max(1, len(keys) // steps)
+            for i, key in enumerate(keys):
+                names[key] = f"{lab}#{i % per_step}"
     agg = collections.defaultdict(lambda: collections.defaultdict(lambda: [0.0, 0]))
     tw = collections.defaultdict(lambda: [0.0, 0])
     for key, c in per.items():
@@ -53,8 +66,10 @@ def load(d):
 
 def main():
     d = sys.argv[1]
-    filt = [a for a in sys.argv[2:] if not a.startswith("--") and not a.endswith(".json")]
-    agg, tw = load(d)
+    skip = {i + 1 for i, a in enumerate(sys.argv) if a in ("--steps", "--json")}
+    filt = [a for i, a in enumerate(sys.argv[2:], 2) if not a.startswith("--") and i not in skip]
+    steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 0
+    agg, tw = load(d, steps)
     out = {}
     for lab, c in sorted(agg.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", [0])[0]):
         if filt and not any(f in lab for f in filt):

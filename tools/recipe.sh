@@ -11,10 +11,15 @@
 #                                                              interleaved twice (tools/bench_layers.py)
 #   bash tools/recipe.sh env      <tag> "<VAR=value>" <layers> <ops>  per-layer A/B under an environment switch
 #   bash tools/recipe.sh benchab  <tag> "<VAR=value>|<lib.so>" [bench args...]   bench A/B, interleaved twice
+#                                                              (BASE=<lib.so>: another baseline than the in-tree one)
 #   bash tools/recipe.sh pmc      <tag> <layers> <ops> "<counters>"  one rocprofv3 --pmc pass over bench_layers
 #   bash tools/recipe.sh isolate  <tag> <test file> "<-k expr>" "<VAR=value>"...   one test under each switch
 #                                                              (baseline first); a test failure does not end the
 #                                                              call, a timeout / crash does
+#   bash tools/recipe.sh benchattrib <tag> <lib.so|""> [bench args...]  tools/pmc_attrib.sh's four counter passes over
+#                                                              one warmup + one timed + one instrumented training step
+#                                                              (post-process: python tools/pmc_attrib.py
+#                                                              gpurun_out/attrib_<tag> --steps 3)
 #   bash tools/recipe.sh mfma     <tag> [bench args...]        MFMA-busy + GRBM_GUI_ACTIVE pass over one bench step
 #                                                              (post-process: python tools/mfma_busy.py <csv>)
 #
@@ -68,7 +73,7 @@ env)
 benchab)
   sw=$1; shift
   for e in "" "$sw" "" "$sw"; do
-    case $e in *.so) envs="CNNITMO_LIB=$e" ;; "") envs="CNNITMO_LIB=$LIB" ;; *) envs=$e ;; esac
+    case $e in *.so) envs="CNNITMO_LIB=$e" ;; "") envs="CNNITMO_LIB=${BASE:-$LIB}" ;; *) envs=$e ;; esac
     echo "== ${e:-baseline}"
     env $envs $T 600 python3 bench.py --no-cpu "$@" 2>> "$O/${tag}_ab.err" | grep -E '^\{' | python3 -c \
       "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['value'], d['ms_per_step'], r['kernel'], r['achieved'])"
@@ -89,6 +94,23 @@ isolate)
     [ $rc -le 1 ] || exit $rc
   done | tee "$O/${tag}_iso.txt"
   rm -f "$O/${tag}_iso.log.tmp" ;;
+benchattrib)
+  lib=${1:-$LIB}; shift
+  case $lib in /*) ;; *) lib=$R/$lib ;; esac
+  A=$O/attrib_$tag
+  mkdir -p "$A"
+  cd /tmp && export TMPDIR=/tmp
+  i=0
+  for ctr in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE" \
+             "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_SALU SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE" \
+             "SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAVES GRBM_GUI_ACTIVE" \
+             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_DATA_FIFO_FULL SQ_LDS_CMD_FIFO_FULL SQ_INST_LEVEL_LDS SQ_INST_LEVEL_VMEM SQ_LDS_UNALIGNED_STALL SQ_INST_CYCLES_VMEM_WR GRBM_GUI_ACTIVE"; do
+    CNNITMO_LIB=$lib timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d "$A/p$i" -o run -- \
+      python3 "$R/bench.py" --no-cpu --steps 1 --warmup 1 --infer-batch 0 --ns-batch 0 --k4-batch 0 \
+      --f32-train-batch 0 "$@" > "$A/p$i.log" 2>&1
+    i=$((i+1))
+  done
+  echo "benchattrib $tag: $i passes" ;;
 mfma)
   cd /tmp && export TMPDIR=/tmp
   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
