@@ -195,3 +195,15 @@ def test_tconv_planner_choices(lib):
         assert name(1, 32, h, w, cin, cout, 1) == b"igemm_fwd2p_kernel<bf16,256x256>"
     assert name(1, 32, 544, 960, 128, 64, 0).startswith(b"tconv_stream_kernel")
     assert name(0, 8, 272, 480, 256, 128, 0).startswith(b"tconv_ws_kernel<f32")  # fp32: unchanged
+
+
+def test_halo_global_accesses_inside_their_tensors():
+    """tools/check_halo_bounds.py: every in-range raw-buffer access of the shipped halo conv
+    (patch and weight pieces, epilogue stores, the fused BN backward's r loads and pool route) of
+    every bench launch shape lies inside the tensor it addresses; the full-line (8 rows x 128 B)
+    patch shape of the round-5 variant that faulted reads past the row (the checker has teeth)."""
+    import tools.check_halo_bounds as hb
+    bad, n = hb.run()
+    assert n > 50 and not bad, bad[:5]
+    bad_line, _ = hb.run(line=128)
+    assert bad_line
