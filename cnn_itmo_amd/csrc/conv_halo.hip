@@ -951,13 +951,9 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
     const char* e = getenv("CNNITMO_HALO");
     return e ? atoi(e) : 1;
   }();
-  // fp32 inference forward: 82.9 -> 94.8 frames/s at 1080p b8, the kernel at 0.87 of fp32
-  // peak against the implicit GEMM's 0.75 (profiles/r03zl_*); CNNITMO_HALO_F32=0 restores it
-  static const int en32 = [] {
-    const char* e = getenv("CNNITMO_HALO_F32");
-    return e ? atoi(e) : 1;
-  }();
-  if (!en || (f32 && !en32)) return false;
+  // (fp32: 82.9 -> 94.8 frames/s at 1080p b8 inference, the kernel at 0.87 of fp32 peak
+  // against the implicit GEMM's 0.75, profiles/r03zl_*)
+  if (!en) return false;
   if (f32) {
     if (a.cin % 16 || a.a_ld % 4 || a.a_off % 4 || a.out_ld % 4 || a.out_off % 4) return false;
     if (a.a2) return false;
@@ -996,11 +992,7 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
     pl.epi = (a.flags || a.bias || a.border || a.stats) ? 1 : 0;
     if (a.a2 && pl.epi != 1) return false;  // two sources: the forward-epilogue kernels only
   }
-  static const int res = [] {
-    const char* e = getenv("CNNITMO_HALO_RES");
-    return e ? atoi(e) : 1;
-  }();
-  pl.res = res && a.cin <= (f32 ? 16 : 32) * RCH;
+  pl.res = a.cin <= (f32 ? 16 : 32) * RCH;
   pl.th = 16;
   return true;
 }

@@ -245,14 +245,7 @@ extern "C" int cnnitmo_bn_apply(int dtype, const void* r, long p, int c, const f
 // ----------------------------------------------------------------------------
 static constexpr int BWD_BLOCKS = 1024;
 
-static int bwd_blocks() {
-  static const int v = [] {
-    const char* e = getenv("CNNITMO_BWD_BLOCKS");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 ? x : BWD_BLOCKS;
-  }();
-  return v;
-}
+static int bwd_blocks() { return BWD_BLOCKS; }
 
 extern "C" int cnnitmo_bn_bwd_rows(long p, int c) {
   (void)c;
@@ -1159,14 +1152,10 @@ template <bool BWD>
 static bool launch_head2(int dtype, const void* x, int n, int h, int h_valid, int w, int cin, const float* wt,
                          const float* b, const float* target, float* yhat, void* dx, float inv_numel,
                          float* part, const float* scale, const float* shift, float* g3, int G_, hipStream_t s) {
-  static const bool en = [] {  // CNNITMO_HEAD2=0: head_kernel (A/B)
-    const char* e = getenv("CNNITMO_HEAD2");
-    return !e || atoi(e) != 0;
-  }();
   const long P = (long)n * h * w;
   const int lpp = cin / (dtype == CNNITMO_BF16 ? 8 : 4);
   // 32-bit pixel and target-byte offsets inside the kernel
-  if (!en || P >= (1L << 30) || (long)n * h_valid * w * 12 >= (1L << 31)) return false;
+  if (P >= (1L << 30) || (long)n * h_valid * w * 12 >= (1L << 31)) return false;
 #define H2K(T, L, G)                                                                                          \
   hipLaunchKernelGGL((head2_kernel<T, L, BWD, G>), dim3(G_), dim3(256), 0, s, (const T*)x, h, h_valid, w, P, wt, \
                      b, target, yhat, (T*)dx, inv_numel, part, scale, shift, g3)

@@ -687,14 +687,7 @@ Cfg2 pick2(int N) {
   return {32};
 }
 
-int stages_for(int bn) {
-  static const int env = [] {
-    const char* e = getenv("CNNITMO_STAGES");
-    return e ? atoi(e) : 0;
-  }();
-  if (env == 2 || env == 3) return env;
-  return bn == 128 ? 3 : 2;
-}
+int stages_for(int bn) { return bn == 128 ? 3 : 2; }
 
 template <typename T, int BM, int BN, int WM, int WN>
 void launch_st(const FwdArgs& a, hipStream_t s, dim3 grid) {
@@ -712,13 +705,9 @@ int fwd2_stat_rows(long m) { return (int)((m + 255) / 256); }
 // other's MFMAs) for the bf16 Conv2DTranspose input gradient (up6/up7 0.87/1.93 ->
 // 0.83/1.81 ms) and for every fp32 launch with N % 128 == 0 (inference dec6-dec8
 // 15.4-15.8 -> 15.0-15.3 ms); launches with BN partial sums keep 256-row tiles (the
-// sums rows are per 256 rows).  CNNITMO_FWD2_BM128=0: 256 everywhere.
+// sums rows are per 256 rows).
 int fwd2_bm(const FwdArgs& a, bool bf16) {
-  static const int en = [] {
-    const char* e = getenv("CNNITMO_FWD2_BM128");
-    return e ? atoi(e) : 1;
-  }();
-  if (!en || a.N % 128 || a.stats) return 256;
+  if (a.N % 128 || a.stats) return 256;
   return (!bf16 || (a.ntaps == 4 && a.scale == 2)) ? 128 : 256;
 }
 bool fwd2_handles(int N) { return N != 32; }
@@ -726,42 +715,30 @@ bool fwd2_handles(int N) { return N != 32; }
 // bf16 Conv2DTranspose input gradient (K = 1024 / 2048): 256 x 256 tiles (8 waves of
 // 128 x 64, 2-deep 128 KB ring, one workgroup per CU) move half the LDS-DMA bytes per
 // MFMA of the 128 x 128 tiles: up6 / up7 0.83 / 1.80 -> 0.70 / 1.66 ms
-// (profiles/r03z_ab_fwd2_256.txt); CNNITMO_FWD2_256=0 restores 128 x 128
+// (profiles/r03z_ab_fwd2_256.txt)
 bool fwd2_t256(const FwdArgs& a, bool bf16) {
-  static const int en = [] {
-    const char* e = getenv("CNNITMO_FWD2_256");
-    return e ? atoi(e) : 1;
-  }();
-  return en && bf16 && a.ntaps == 4 && a.scale == 2 && a.N % 256 == 0 && !a.stats;
+  return bf16 && a.ntaps == 4 && a.scale == 2 && a.N % 256 == 0 && !a.stats;
 }
 
 // ... as the persistent kernel (igemm_fwd2p_kernel) for the input-gradient geometry when
-// nothing is asked of the epilogue but the store; CNNITMO_FWD2_PERS=0: the one-tile-per-workgroup launch
+// nothing is asked of the epilogue but the store (others: the one-tile-per-workgroup launch)
 bool fwd2_pers(const FwdArgs& a, bool bf16) {
-  static const int en = [] {
-    const char* e = getenv("CNNITMO_FWD2_PERS");
-    return e ? atoi(e) : 1;
-  }();
-  return en && fwd2_t256(a, bf16) && !a.scatter && !a.border && !a.bias && !a.flags &&
+  return fwd2_t256(a, bf16) && !a.scatter && !a.border && !a.bias && !a.flags &&
          a.hs == 2 * a.ho && a.ws == 2 * a.wo && a.cin % 64 == 0 && a.dyc == 0xa5 && a.dxc == 0x99 && !a.cin1 && a.M < (1L << 31) &&
          (2L * (256 / a.wo + 2) + 2) * a.ws * a.a_ld * 2 < (1L << 31);  // (a tile's source span: 32-bit offsets)
 }
 
 static int cu_count();
 // the bf16 Conv2DTranspose forward (bias or folded per-column bias, ReLU, inference affine,
-// BN partial sums) on tconv_fwd2p_kernel; CNNITMO_TFWD2P=0: tconv_ws / tconv_stream.  The plan
+// BN partial sums) on tconv_fwd2p_kernel (others: tconv_stream / tconv_ws).  The plan
 // (tfwd2p_handles) depends on the sizes and flags only, so cnnitmo_tconv2x2_stat_rows (which asks
 // it with dense views) always sizes the stats buffer for the kernel the launch will run; the view
 // conditions (16-byte alignment, 32-bit buffer offsets of the strides) are not part of the plan
 // but requirements of the launch: a view that fails them is an error, never a silent fall-back to
 // a kernel with a different stat-row count.
 bool tfwd2p_handles(const FwdArgs& a, bool bf16) {
-  static const int en = [] {
-    const char* e = getenv("CNNITMO_TFWD2P");
-    return e ? atoi(e) : 1;
-  }();
   const int gx = std::max(cu_count() / 8, 1);
-  return en && bf16 && a.scatter && a.ntaps == 1 && a.N % 256 == 0 && a.cin % 64 == 0 && a.cout % 8 == 0 &&
+  return bf16 && a.scatter && a.ntaps == 1 && a.N % 256 == 0 && a.cin % 64 == 0 && a.cout % 8 == 0 &&
          !a.border && !(a.flags & ~(CNNITMO_RELU | CNNITMO_STATS | CNNITMO_BIAS_PER_COL | CNNITMO_AFFINE)) &&
          a.M < (1L << 31) && gx % (a.N / 256) == 0;
 }

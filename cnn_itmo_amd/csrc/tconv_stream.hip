@@ -159,22 +159,65 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
     apx[i] = row & 63;
     apc[i] = (lane & 3) ^ (((row >> 2) & 1) << 1);
   }
-  // tile -> (img, y, x0)
-  auto tile_pos = [&](long t, int& img, int& y, int& x0) {
-    const int tx = (int)(t % p.tiles_x);
-    const long ry = t / p.tiles_x;
-    y = (int)(ry % p.h);
-    img = (int)(ry / p.h);
-    x0 = tx * 64;
+  // Item positions advance incrementally (one item = (tile, chunk); tiles are consecutive,
+  // image -> row -> 64-pixel strip): the 64-bit divisions of a per-item tile_pos were ~250
+  // scalar instructions per item, issued in front of every stage's DMA.
+  struct It {
+    int kc, tl, tx, y, img;  // chunk, tile (relative to t0), strip, row, image
+    int tap[2], co[2];       // MODE 1: the K step of each of the wave's two DMA rows (its tap, channel)
+  };
+  auto it_init = [&](It& s) {
+    const int tx = (int)(t0 % p.tiles_x);
+    const long ry = t0 / p.tiles_x;
+    s.kc = 0;
+    s.tl = 0;
+    s.tx = tx;
+    s.y = (int)(ry % p.h);
+    s.img = (int)(ry / p.h);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {  // k = kc * 128 + aks * 32 (wave-uniform: aks is the row's 64-block)
+      const int k = __builtin_amdgcn_readfirstlane(aks[i] * 32);
+      s.tap[i] = MODE == 1 ? k / p.cout : 0;
+      s.co[i] = MODE == 1 ? k - s.tap[i] * p.cout : 0;
+    }
+  };
+  auto it_next = [&](It& s) {
+    if (++s.kc < nch) {
+      if constexpr (MODE == 1) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // k += 128 (cout % 32 == 0)
+          s.co[i] += 128;
+          while (s.co[i] >= p.cout) {
+            s.co[i] -= p.cout;
+            ++s.tap[i];
+          }
+        }
+      }
+      return;
+    }
+    s.kc = 0;
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int k = __builtin_amdgcn_readfirstlane(aks[i] * 32);
+        s.tap[i] = k / p.cout;
+        s.co[i] = k - s.tap[i] * p.cout;
+      }
+    }
+    ++s.tl;
+    if (++s.tx < p.tiles_x) return;
+    s.tx = 0;
+    if (++s.y < p.h) return;
+    s.y = 0;
+    ++s.img;
   };
   const int W2 = 2 * p.w;
 
-  // item q = (tile, chunk); loads: A chunk (+ R tile with the last chunk, EPI)
-  auto issue = [&](long q, int slot) -> int {
-    const long t = t0 + q / nch;
-    const int kc = (int)(q % nch);
-    int img, y, x0;
-    tile_pos(t, img, y, x0);
+  // the next item (tile, chunk) of the ring; loads: A chunk (+ R tile with the last chunk, EPI)
+  It iss;
+  it_init(iss);
+  auto issue = [&](int slot) -> int {
+    const int kc = iss.kc, img = iss.img, y = iss.y, x0 = iss.tx * 64;
     char* S = ring + slot * STAGE;
     if constexpr (MODE == 0) {
       const i32x4 rs = dma::rsrc((uintptr_t)(p.a + (((size_t)img * p.h + y) * p.w + x0) * p.a_ld + p.a_off + kc * 128));
@@ -187,8 +230,7 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
       const i32x4 rs = dma::rsrc((uintptr_t)(p.a + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.cout));
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const int k = kc * 128 + aks[i] * 32;  // 32 | cout: the step lies in one tap
-        const int tap = k / p.cout, co = k - tap * p.cout;
+        const int tap = iss.tap[i], co = iss.co[i];  // 32 | cout: the step lies in one tap
         const bool ok = x0 + apx[i] < p.w;
         const unsigned off = (unsigned)((((tap >> 1) * W2 + 2 * apx[i] + (tap & 1)) * p.cout + co + apc[i] * 8) * 2);
         dma::lds16(ok ? off : OOB, rs, S + (wave * 2 + i) * 1024);
@@ -197,7 +239,7 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
     int n = 2;
     if constexpr (EPI) {
       if (kc == nch - 1) {  // the producer's r tile [64 px][BN] for the fused BN backward
-        char* R = rr + (int)((q / nch) & 1) * C::RSLOT;
+        char* R = rr + (iss.tl & 1) * C::RSLOT;
         const i32x4 rs = dma::rsrc((uintptr_t)(p.r + (((size_t)img * p.h + y) * p.w + x0) * p.r_ld + p.r_off + n0));
         for (int j = wave; j < 64 * PPR / 64; j += 8) {  // 1 KB instructions
           const int slot16 = j * 64 + lane, px = slot16 / PPR, sl = slot16 - px * PPR;
@@ -208,6 +250,7 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
         n += (64 * PPR / 64 + 7 - wave) / 8;
       }
     }
+    it_next(iss);
     return n;
   };
 
@@ -258,9 +301,8 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   for (int j = 0; j < FP; ++j)
 #pragma unroll
     for (int k = 0; k < 8; ++k) s1[j][k] = s2[j][k] = 0.f;
-  auto epilogue = [&](long t, int rslot) {
-    int img, y, x0;
-    tile_pos(t, img, y, x0);
+  auto epilogue = [&](const It& e, int rslot) {
+    const int img = e.img, y = e.y, x0 = e.tx * 64;
     if constexpr (MODE == 0) {
       const __amdgpu_buffer_rsrc_t os =
           srsrc(p.out + (((size_t)img * 2 * p.h + 2 * y) * W2 + 2 * x0) * p.out_ld + p.out_off);
@@ -335,26 +377,29 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   int mq[ST];
 #pragma unroll
   for (int k = 0; k < ST - 1; ++k) {
-    if (k < T) issued += issue(k, k);
+    if (k < T) issued += issue(k);
     mq[k] = issued;
   }
   mq[ST - 1] = issued;
   int slot = 0;
+  It cur;  // the item being computed
+  it_init(cur);
   for (long q = 0; q < T; ++q) {
     dma::wait_vm_dyn(issued - mq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     if (q + ST - 1 < T) {
-      issued += issue(q + ST - 1, slot == 0 ? ST - 1 : slot - 1);
+      issued += issue(slot == 0 ? ST - 1 : slot - 1);
       mq[ST - 1] = issued;
     }
-    const int kc = (int)(q % nch);
+    const int kc = cur.kc;
     compute(slot, kc);
     if (kc == nch - 1) {
-      epilogue(t0 + q / nch, (int)((q / nch) & 1));
+      epilogue(cur, cur.tl & 1);
       issued += S;
     }
+    it_next(cur);
 #pragma unroll
     for (int k = 0; k < ST - 1; ++k) mq[k] = mq[k + 1];
     slot = slot == ST - 1 ? 0 : slot + 1;
@@ -393,11 +438,7 @@ struct TSPlan {
 };
 
 bool ts_plan(int mode, int h, int w, int cin, int cout, bool epi, TSPlan& pl) {
-  static const int en = [] {
-    const char* e = getenv("CNNITMO_TCONV_STREAM");
-    return e ? atoi(e) : 1;
-  }();
-  if (!en || w < 1 || h < 1) return false;
+  if (w < 1 || h < 1) return false;
   const int K = mode == 0 ? cin : 4 * cout, N = mode == 0 ? 4 * cout : cin;
   if (K % 128 || cout % 32 || N % 64) return false;
   int bn = 64 * 1024 / (K * 2);  // the resident weight block: K x BN bf16 <= 64 KB

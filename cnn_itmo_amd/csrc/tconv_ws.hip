@@ -359,17 +359,9 @@ struct WSPlan {
 };
 
 bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
-  static const int en = [] {
-    const char* e = getenv("CNNITMO_TCONV_WS");
-    return e ? atoi(e) : 1;
-  }();
-  // fp32 inference forward (up6-up8): 0.61-0.69 -> 0.79-0.80 of fp32 peak, 1080p b8 fp32
-  // inference 94.3 -> 95.9 frames/s (profiles/r03zp_*); CNNITMO_TCONV_WS_F32=0 restores the GEMM
-  static const int en32 = [] {
-    const char* e = getenv("CNNITMO_TCONV_WS_F32");
-    return e ? atoi(e) : 1;
-  }();
-  if (!en || cout % 32 || cin % 32) return false;
+  // (fp32 inference forward, up6-up8: 0.61-0.69 -> 0.79-0.80 of fp32 peak against the
+  // implicit GEMM, 1080p b8 fp32 inference 94.3 -> 95.9 frames/s, profiles/r03zp_*)
+  if (cout % 32 || cin % 32) return false;
   // the bf16 input gradient (up8, K = 512) runs on igemm_fwd2p_kernel: 1.52 -> 1.31 ms
   // (profiles/r05/r05t2_ab_up8_dgrad_fwd2p.txt)
   if (mode == 1 && !f32) return false;
@@ -378,7 +370,7 @@ bool ws_plan(int mode, int cin, int cout, WSPlan& pl, bool f32 = false) {
     // K = 128 is up9 (128 -> 64 channels at full resolution), which ran on igemm_fwd2's
     // 128 x 128 tiles at 0.49 of fp32 peak (a 256-column block spills: 16 fp32 fragments).
     // fp32 input gradient (training): K = 4 * cout = 256 (up9) / 512 (up8)
-    if (!en32 || (K != 128 && K != 256 && K != 512) || (mode == 1 && K == 128)) return false;
+    if ((K != 128 && K != 256 && K != 512) || (mode == 1 && K == 128)) return false;
     const int bn = K == 512 ? 64 : 128;
     if (N % bn || N / bn > 32 || 32 % (N / bn)) return false;
     pl.bn = bn;

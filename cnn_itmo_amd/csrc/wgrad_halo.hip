@@ -606,32 +606,15 @@ struct WHPlan {
 };
 
 bool wh_plan(int n, int h, int w, int cin, int cout, WHPlan& pl, bool cat = false) {
-  static const int mode = [] {
-    const char* e = getenv("CNNITMO_WGRAD_HALO");
-    return e ? atoi(e) : 1;
-  }();
-  if (!mode) return false;
   pl.bm = cout % 64 == 0 ? 64 : (cout == 32 ? 32 : 0);
-  static const int bn128 = [] {
-    const char* e = getenv("CNNITMO_WH_BN128");
-    return e ? atoi(e) : 2;
-  }();
   pl.bn = cin % 96 == 0 ? 96 : (cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0));
-  if (!cat && cout % 64 == 0 && cin % 128 == 0 && (bn128 >= 2 || (bn128 == 1 && pl.bn != 96))) pl.bn = 128;
-  static const int split192 = [] {
-    const char* e = getenv("CNNITMO_WH_SPLIT192");
-    return e ? atoi(e) : 1;
-  }();
-  pl.split = !cat && split192 && cin == 192 && cout % 64 == 0;
+  if (!cat && cout % 64 == 0 && cin % 128 == 0) pl.bn = 128;
+  pl.split = !cat && cin == 192 && cout % 64 == 0;
   if (pl.split) pl.bn = 128;  // (the planner below sizes the 128-column launch; the 64 one follows it)
   if (!pl.bm || !pl.bn) return false;
   // 128-column strips also when w % 128 != 0 (a partial last strip): enc2a at 960
-  // columns 1.12 -> 0.99 ms (tools/ab_env.sh); CNNITMO_WH_TW128=0 restores 64
-  static const int tw128 = [] {
-    const char* e = getenv("CNNITMO_WH_TW128");
-    return e ? atoi(e) : 1;
-  }();
-  pl.tw = (pl.bm * pl.bn <= 32 * 64 && (w % 128 == 0 || (tw128 && w % 64 == 0))) ? 128 : 64;
+  // columns 1.12 -> 0.99 ms
+  pl.tw = (pl.bm * pl.bn <= 32 * 64 && w % 64 == 0) ? 128 : 64;
   pl.strips = (w + pl.tw - 1) / pl.tw;  // a partial last strip reads zero columns
   pl.cbm = cout / pl.bm;
   pl.cbn = pl.split ? 1 : cin / pl.bn;
@@ -686,11 +669,6 @@ void wh_launch(const WHArgs& a, unsigned grid, hipStream_t s) {
 // fp32 plan: 32 / 64 x 32 / 64 blocks (64 x 96 for cin 96), 64-pixel strips, the row split of
 // wh_plan's policy
 bool wh_plan_f32(int n, int h, int w, int cin, int cout, WHPlan& pl) {
-  static const int mode = [] {
-    const char* e = getenv("CNNITMO_WGRAD_HALO_F32");
-    return e ? atoi(e) : 1;
-  }();
-  if (!mode) return false;
   pl.bm = cout % 64 == 0 ? 64 : (cout % 32 == 0 ? 32 : 0);
   pl.bn = cin % 64 == 0 ? 64 : (cin % 32 == 0 ? 32 : 0);
   if (WF_BN96 && pl.bm == 64 && cin % 96 == 0 && cin % 64 != 0) pl.bn = 96;

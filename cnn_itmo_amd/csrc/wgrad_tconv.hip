@@ -211,11 +211,6 @@ struct WTPlan {
 };
 
 bool wt_plan(int n, int h, int w, int cin, int cout, WTPlan& pl) {
-  static const int mode = [] {
-    const char* e = getenv("CNNITMO_TCONV_WGRAD");
-    return e ? atoi(e) : 1;
-  }();
-  if (!mode) return false;
   pl.bm = cout % 128 == 0 ? 128 : (cout % 64 == 0 ? 64 : 0);
   pl.bn = cin % 128 == 0 ? 128 : 0;
   if (!pl.bm || !pl.bn) return false;
@@ -411,11 +406,7 @@ __global__ __launch_bounds__(WTF_NW * 64) void wgrad_tconv_f32_kernel(const WTFA
 
 // row split for the fp32 kernel: the bf16 plan's policy at one 120 KB workgroup per CU
 bool wtf_plan(int n, int h, int w, int cin, int cout, WTPlan& pl) {
-  static const int mode = [] {
-    const char* e = getenv("CNNITMO_TCONV_WGRAD");
-    return e ? atoi(e) : 1;
-  }();
-  if (!mode || cout % WTF_BM || cin % WTF_BN) return false;
+  if (cout % WTF_BM || cin % WTF_BN) return false;
   pl.bm = WTF_BM;
   pl.bn = WTF_BN;
   pl.strips = (w + WTF_TW - 1) / WTF_TW;

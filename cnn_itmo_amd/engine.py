@@ -24,15 +24,12 @@ affine: convs/tconvs fold it into their weights and bias each step
 it on load, and the consumer's weight gradient gets the exact correction
 s*dW(r) + h*V (cnnitmo_conv_wgrad / tconv2x2_wgrad fold arguments).  This
 removes one read+write of every activation per step.  Dropout outputs stay
-materialised (identity coefficients).  CNNITMO_NO_FOLD=1 disables folding.
+materialised (identity coefficients).
 Every parameter lives in one flat fp32 buffer laid out in REVERSE stage order,
 so backward produces gradients front-to-back -- the order the data-parallel
 bucketer (dist.py) all-reduces them in.
 """
 from __future__ import annotations
-
-import contextlib
-import os
 
 import numpy as np
 import torch
@@ -185,9 +182,9 @@ class BlockStage(Stage):
             self.w_fwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
             self.w_bwd = torch.empty(4 * cout * cin, dtype=T, device=dev)
         self.foldable = self.kind != "c3in" and self.vin.folded
-        # first layer without im2col (32 filters; CNNITMO_C3_DIRECT=0: im2col + 1-tap GEMM):
+        # first layer without im2col (32 filters; other widths: im2col + 1-tap GEMM):
         # both dtypes run conv_c3's forward and weight gradient, training and inference
-        self.direct_ok = (self.kind == "c3in" and cout == 32 and os.environ.get("CNNITMO_C3_DIRECT", "1") != "0")
+        self.direct_ok = self.kind == "c3in" and cout == 32
         self.direct = self.direct_ok
         if self.foldable:  # per-step folded copies (training)
             f32 = torch.float32
@@ -401,7 +398,6 @@ class BlockStage(Stage):
             v = self.vout
             if v.sum_consumers and len(v.bn_contrib) == v.sum_consumers:
                 # sums from the consumers' weight gradients (cnnitmo_bn_consumer_sums): no pass over dy
-                e.join_side(keep=True)
                 part = torch.cat(v.bn_contrib)
                 prow = part.numel() // (2 * cout)
             else:
@@ -447,7 +443,7 @@ class BlockStage(Stage):
         """The (value, channel offset) among `targets` whose BN backward this stage's dgrad
         applies (cnnitmo_conv3x3_dgrad_bn), with its partial-sum row count; or None."""
         e = self.eng
-        if self.kind not in ("c3", "t2") or not e.fuse_bnb or not self.vin.needs_grad:
+        if self.kind not in ("c3", "t2") or not self.vin.needs_grad:
             return None
         for m, ci0 in targets:
             if m.fuse_into is self and m.sum_consumers == 1:
@@ -467,10 +463,8 @@ class BlockStage(Stage):
     def _skip_member(self, ci0):
         """The concat member holding input channels [0, ci0) when it is exactly one value
         without a gradient yet (dec9's `conv1`, 64 B of every 192-B row): the split dgrad
-        then writes its gradient to a dense buffer of its own (CNNITMO_DENSE_SKIP=0: into
-        the concat's gradient slice).  Nothing reads that gradient through the concat."""
-        if os.environ.get("CNNITMO_DENSE_SKIP", "1") == "0":
-            return None
+        then writes its gradient to a dense buffer of its own.  Nothing reads that gradient
+        through the concat."""
         ms = [v for v in self.vin.members if v.place and v.place[1] < ci0]
         if len(ms) == 1 and ms[0].place[1] == 0 and ms[0].c == ci0 and not ms[0].ginit:
             return ms[0]
@@ -481,12 +475,10 @@ class BlockStage(Stage):
         pool1 and its BN-backward sums come from its consumers, its input gradient is not
         launched here but inside conv1's BN backward, where pool1's gradient is routed in
         (cnnitmo_conv3x3_dgrad_bn_pooled): the 32-channel skip gradient is neither written
-        nor read back, and the stand-alone pooled BN-backward apply disappears.
-        CNNITMO_DEFER_SKIP=0: the separate dgrad + bn_bwd_apply_pooled; =dec9: dec9 only.
-        (_split_fused splits dec7's and dec8's input gradients for the same purpose.)"""
+        nor read back, and the stand-alone pooled BN-backward apply disappears (otherwise: the
+        separate dgrad + bn_bwd_apply_pooled).  (_split_fused splits dec7's and dec8's input
+        gradients for the same purpose.)"""
         e = self.eng
-        if os.environ.get("CNNITMO_DEFER_SKIP", "1") == "0" or not e.fuse_bnb:
-            return False
         prod = skip.producer
         if prod is None or prod.bn is None or prod.drop is not None or not skip.folded or skip.sum_consumers != 2:
             return False
@@ -502,13 +494,11 @@ class BlockStage(Stage):
         48-column blocks whose epilogue straddles both (measured 15 ms); its skip part is a
         plain dgrad, or deferred (_defer_skip).  dec7 / dec8 (model.py:251, 256): when the
         skip member's gradient is deferred into its producer's BN backward with its pool's
-        route (CNNITMO_DEFER_SKIP=1; "dec9": dec9 only).  CNNITMO_SPLIT_DGRAD=0: one launch."""
-        if not (ci0 > 0 and ci0 + c == self.cin and ci0 % 32 == 0 and os.environ.get("CNNITMO_SPLIT_DGRAD", "1") != "0"):
+        route.  Otherwise: one launch."""
+        if not (ci0 > 0 and ci0 + c == self.cin and ci0 % 32 == 0):
             return False
         if self.cin % 64 != 0 and c % 64 == 0:
             return True
-        if os.environ.get("CNNITMO_DEFER_SKIP", "1") != "1":
-            return False
         skip = self._skip_member(ci0)
         return skip is not None and self._defer_skip(skip, n)
 
@@ -524,52 +514,46 @@ class BlockStage(Stage):
             ops.colsum(part2, rows, 4 * cout, 1, psum)
         else:
             ops.colsum(part2, rows, cout, 1, db)
-        # The weight gradient is off the critical path (dz -> dgrad -> next BN backward).
-        # With CNNITMO_SIDE_STREAM=1 it runs on a side stream beside the compute stream's
-        # dgrad and BN passes; off by default: every kernel here is persistent (one
-        # workgroup per CU), so the two streams only interleave whole CUs, and the bench
-        # measured 195.8 (one stream) vs 195.6 frames/s (profiles/r03c_*), while each
-        # side-stream kernel ran up to 3x slower in the step than alone.
+        # The weight gradient is off the critical path (dz -> dgrad -> next BN backward), but
+        # it stays on the compute stream: every kernel here is persistent (one workgroup per
+        # CU), so a side stream only interleaves whole CUs; it measured 195.8 (one stream) vs
+        # 195.6 frames/s (profiles/r03c_*) and was removed in round 6.
         targets = self._sum_targets() if self.fold_active else []
         fz = self._fused_target(n, targets)
-        # with a fused producer BN the dgrad needs this weight gradient's sums first
-        ctx = contextlib.nullcontext() if fz else e.side(dz, psum, getattr(self, "cols", None),
-                                                         e.x_in if self.direct else None)
-        with ctx:
-            raw = torch.empty_like(dw) if targets else None
-            if self.kind == "c3in" and self.direct:
-                ops.conv_c3_wgrad(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, dz, dw)
-            elif self.kind == "c3in":
-                ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
-                               dw, dw_cols=27)
-            elif self.kind == "c3":
-                fold = None
-                if self.fold_active:
-                    h, w = self.vout.h, self.vout.w
-                    brows = ops.border_rows(n)
-                    bpart = torch.empty(brows * 8 * cout, device=e.device, dtype=torch.float32)
-                    ops.border_sums(e.dt, dz, n, h, w, cout, bpart)
-                    bsum = torch.empty(8 * cout, device=e.device, dtype=torch.float32)
-                    ops.colsum(bpart, brows, 8 * cout, 1, bsum)
-                    fold = self.vin.coef() + (db, bsum)
-                if self.vin.split:
-                    a, b = self.vin.members
-                    ops.conv_wgrad_cat(e.dt, a.view(n), b.view(n), dz, cout, dw, fold=fold, raw=raw)
-                else:
-                    ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
-                for m, ci0 in targets:
-                    pm = torch.empty(L.CONSUMER_ROWS * 2 * m.c, device=e.device, dtype=torch.float32)
-                    ops.bn_consumer_sums(1, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, db,
-                                         bsum, m.producer.smean, m.producer.sinv, pm)
-                    m.bn_contrib.append(pm)
+        raw = torch.empty_like(dw) if targets else None
+        if self.kind == "c3in" and self.direct:
+            ops.conv_c3_wgrad(e.dt, e.x_in, n, e.h_valid, self.vout.h, self.vout.w, dz, dw)
+        elif self.kind == "c3in":
+            ops.conv_wgrad(e.dt, 1, ops.View(self.cols, n, self.vout.h, self.vout.w, 32, 32), dz, cout,
+                           dw, dw_cols=27)
+        elif self.kind == "c3":
+            fold = None
+            if self.fold_active:
+                h, w = self.vout.h, self.vout.w
+                brows = ops.border_rows(n)
+                bpart = torch.empty(brows * 8 * cout, device=e.device, dtype=torch.float32)
+                ops.border_sums(e.dt, dz, n, h, w, cout, bpart)
+                bsum = torch.empty(8 * cout, device=e.device, dtype=torch.float32)
+                ops.colsum(bpart, brows, 8 * cout, 1, bsum)
+                fold = self.vin.coef() + (db, bsum)
+            if self.vin.split:
+                a, b = self.vin.members
+                ops.conv_wgrad_cat(e.dt, a.view(n), b.view(n), dz, cout, dw, fold=fold, raw=raw)
             else:
-                fold = self.vin.coef() + (psum,) if par else None
-                ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
-                for m, ci0 in targets:
-                    pm = torch.empty(L.CONSUMER_ROWS * 2 * m.c, device=e.device, dtype=torch.float32)
-                    ops.bn_consumer_sums(2, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, None,
-                                         psum, m.producer.smean, m.producer.sinv, pm)
-                    m.bn_contrib.append(pm)
+                ops.conv_wgrad(e.dt, 9, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
+            for m, ci0 in targets:
+                pm = torch.empty(L.CONSUMER_ROWS * 2 * m.c, device=e.device, dtype=torch.float32)
+                ops.bn_consumer_sums(1, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, db,
+                                     bsum, m.producer.smean, m.producer.sinv, pm)
+                m.bn_contrib.append(pm)
+        else:
+            fold = self.vin.coef() + (psum,) if par else None
+            ops.tconv_wgrad(e.dt, self.vin.view(n), dz, cout, dw, fold=fold, raw=raw)
+            for m, ci0 in targets:
+                pm = torch.empty(L.CONSUMER_ROWS * 2 * m.c, device=e.device, dtype=torch.float32)
+                ops.bn_consumer_sums(2, e.p(self.conv.name + "/kernel"), raw, cout, self.cin, ci0, m.c, None,
+                                     psum, m.producer.smean, m.producer.sinv, pm)
+                m.bn_contrib.append(pm)
         if fz is not None:
             m, ci0, frows = fz
             prod = m.producer
@@ -708,12 +692,11 @@ class HeadStage(Stage):
     def _rank3(self):
         """The producer's BN backward can take the head's input gradient as its rank-3
         factor g3 (dy = g3 . W): a folded BN output (sums from the head's raw sums),
-        no Dropout, consumed by the head alone.  CNNITMO_HEAD_G3=0: store dy."""
+        no Dropout, consumed by the head alone."""
         v, e = self.vin, self.eng
         prod = v.producer
         return (e.training and v.folded and v.sum_consumers == 1 and not v.place and prod is not None
-                and prod.bn is not None and prod.drop is None and prod.kind == "c3"
-                and os.environ.get("CNNITMO_HEAD_G3", "1") != "0")
+                and prod.bn is not None and prod.drop is None and prod.kind == "c3")
 
     def loss_and_grad(self, n, target, loss_acc, grad_numel=0.0):
         """grad_numel: the MSE gradient's normaliser (0: this batch's element count)."""
@@ -909,7 +892,7 @@ class Engine:
         self.dtype_name = dtype
         self.dt, self.tdtype = ops.DTYPES[dtype]
         self.device = torch.device(device)
-        self.stages = compile_graph(model, fold=os.environ.get("CNNITMO_NO_FOLD", "0") != "1")
+        self.stages = compile_graph(model)
         self._plan_split_concats()
         self._plan_pool_fusion()
         self._plan_head_fusion()
@@ -930,11 +913,6 @@ class Engine:
         self.step = 0
         self.grad_hook = None  # callable(lo, hi) after each stage's gradients are written
         self.fwd_hook = None  # callable() after the training forward (moving stats final)
-        self._side = None  # side stream for weight gradients (CNNITMO_SIDE_STREAM=1: on)
-        self._side_on = os.environ.get("CNNITMO_SIDE_STREAM", "0") == "1"
-        # consumer dgrads apply their producer's BN backward (CNNITMO_FUSE_BNB=0: separate pass)
-        self.fuse_bnb = os.environ.get("CNNITMO_FUSE_BNB", "1") != "0"
-        self._side_keep = []
 
     def _plan_split_concats(self):
         """Keep the members of a concatenate in dense buffers of their own when their
@@ -944,9 +922,8 @@ class Engine:
         BN-backward apply read conv1 in half lines and up9 writes them.  Its consumer
         (conv9, a 3x3 conv, model.py:262) then reads both members directly: cnnitmo_conv3x3_fwd_cat /
         cnnitmo_conv_wgrad_cat (bf16 halo kernels; its input gradient is already split
-        per member).  CNNITMO_SPLIT_CAT=0, or sizes either entry point rejects: one
-        concat buffer."""
-        if self.dt != L.BF16 or os.environ.get("CNNITMO_SPLIT_CAT", "1") == "0":
+        per member).  Sizes either entry point rejects: one concat buffer."""
+        if self.dt != L.BF16:
             return
         readers = {}
         for st in self.stages:
@@ -979,10 +956,8 @@ class Engine:
         consumers) and pools r by sign(gamma); the pooled value is then a folded value too,
         with the producer's BN coefficients (Value.coef_src), and its consumer conv folds them
         like any other.  Needs: a 'c3' producer with BN and no Dropout (Dropout outputs are
-        materialised by bn_apply), BN folding on, the halo kernel for the producer's sizes.
-        CNNITMO_POOL_FUSE=0: the stand-alone pool kernel."""
-        if os.environ.get("CNNITMO_POOL_FUSE", "1") == "0":
-            return
+        materialised by bn_apply), BN folding on, the halo kernel for the producer's sizes
+        (otherwise the stand-alone pool kernel)."""
         for st in self.stages:
             if not isinstance(st, PoolStage):
                 continue
@@ -1003,9 +978,7 @@ class Engine:
         feeds it (conv9, model.py:262): predict() then never stores that conv's 64-channel
         output (fp32 b8 at 1080p: 4.3 GB written and read back).  Needs: a 'c3' producer with
         BN and no Dropout / pooling / concat, consumed by the head alone, 64 channels, the halo
-        kernel for its sizes.  CNNITMO_HEAD_FUSE=0: the stand-alone head kernel."""
-        if os.environ.get("CNNITMO_HEAD_FUSE", "1") == "0":
-            return
+        kernel for its sizes (otherwise the stand-alone head kernel)."""
         head = self.stages[-1]
         if not isinstance(head, HeadStage):
             return
@@ -1063,28 +1036,6 @@ class Engine:
                 if isinstance(st, BlockStage):
                     st.prep()
             self.weights_dirty = False
-
-    # ---- streams -------------------------------------------------------------
-    def side(self, *tensors):
-        """Context running its work on the side stream after everything queued so far
-        on the compute stream; `tensors` (allocated on the compute stream) are kept
-        alive for it.  Without a side stream: a no-op context."""
-        if not self._side_on:
-            return contextlib.nullcontext()
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        main = torch.cuda.current_stream(self.device)
-        self._side.wait_stream(main)
-        # keep the inputs alive until join_side() instead of record_stream(): deferred
-        # frees of multi-GB blocks would defeat the caching allocator's reuse
-        self._side_keep.extend(t for t in tensors if t is not None)
-        return torch.cuda.stream(self._side)
-
-    def join_side(self, keep=False):
-        if self._side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self._side)
-        if not keep:
-            self._side_keep.clear()
 
     # ---- execution ----------------------------------------------------------
     def _input(self, x):
@@ -1152,16 +1103,13 @@ class Engine:
         head = self.stages[-1]
         gn = 0.0 if grad_frames is None else float(grad_frames) * self.h_valid * self.model.inputs[0].shape[1] * 3
         head.loss_and_grad(n, target.contiguous().float(), loss_acc, gn)
-        if self.grad_hook:
-            with self.side():  # hooks (DP all-reduce launches) follow both streams' writes
-                self.grad_hook(*self.stage_goff[-1])
+        if self.grad_hook:  # (DP all-reduce launches behind the stage's gradient writes)
+            self.grad_hook(*self.stage_goff[-1])
         for i in range(len(self.stages) - 2, -1, -1):
             st = self.stages[i]
             st.backward(n)
             if self.grad_hook and st.params:
-                with self.side():
-                    self.grad_hook(*self.stage_goff[i])
-        self.join_side()
+                self.grad_hook(*self.stage_goff[i])
         self._release()
         if sync is not None:
             sync()
