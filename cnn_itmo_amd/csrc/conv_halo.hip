@@ -121,16 +121,21 @@ struct HaloArgs {
 // and s * (min r) + h where gamma < 0: the kernel pools r by the per-channel mode sign(gamma)
 // (pool_sign), and the pooled value is itself a folded value.  Inference stores y (AFFINE)
 // and pools it by its maximum.
-// NOSUM (EPI 1): no BN partial sums (the inference forward): the 2 x FP x 8 accumulators live across
-// the whole launch otherwise
+// ALT, EPI 1 (NOSUM): no BN partial sums (the inference forward): the 2 x FP x 8 accumulators live
+// across the whole launch otherwise.  ALT, EPI 2 (ALLF): every column is BN-fused (c0 = 0, c1 = N:
+// every fused dgrad of the model but dec6's): the epilogue has no per-column branch.  A per-lane
+// `fused` test in the value loop compiles to an exec-mask branch per value (about ten scalar
+// instructions each, 91 such branches per epilogue); the ALLF epilogue stores through raw-buffer
+// offsets from the wave's first pixel.
 // POOL (EPI 2): the deferred MaxPooling2D backward of the producer's output rides on the fused BN
 // backward (cnnitmo_conv3x3_dgrad_bn_pooled): every column is BN-fused, and the gradient the
 // dgrad computes (the concat skip path) is first increased by the pooled gradient routed to this
 // pixel by the window indices (pool_out = dy_pool, pool_idx; the pool's [n][ho/2][wo/2][N]).  A
 // wave's two tile rows are one row of 2x2 windows, so a lane's window position is
 // (tile row, pixel-column parity) and the pooled row it reads is shared by both rows.
-template <typename TE, int BN, int EPI, bool RES, bool POOL = false, int THT = 16, bool NOSUM = false>
+template <typename TE, int BN, int EPI, bool RES, bool POOL = false, int THT = 16, bool ALT = false>
 __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
+  constexpr bool NOSUM = EPI == 1 && ALT, ALLF = EPI == 2 && ALT;
   using C = HCfg<BN, RES, THT>;
   constexpr int TH = THT, RPW = TH / NWAVE, FM = RPW * FMR, PROWS = (TH + 2) * PW;  // (shadow the 16-row defaults)
   constexpr int PPC = C::PPC, NPI = C::NPI;
@@ -644,11 +649,13 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
 #pragma unroll
     for (int q = 0; q < FP; ++q) {
       const int cl = 32 * q + 8 * g, c = n0 + cl;
-      const bool fz = c >= c0 && c < c1;
+      const bool fz = ALLF || (c >= c0 && c < c1);
       float ca[8], cb[8], ce[8];
       lds8(par + cl, ca);
       lds8(par + BN + cl, cb);
       lds8(par + 2 * BN + cl, ce);
+      // ALLF: dz of the pair's columns at the wave's first pixel (c0 = 0, cbn = N)
+      const __amdgpu_buffer_rsrc_t zs = dma::brsrc(ALLF ? (const void*)(Z + m0 * cbn + n0 + 32 * q) : (const void*)Z);
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
@@ -675,11 +682,16 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
             o[k] = from_f32<bf16>(gk);
           }
         }
-        const long m = m0 + (long)rr * p.wo + col;
-        uint4* dst = !ok ? h_sink + lane
-                     : fz ? reinterpret_cast<uint4*>(Z + (size_t)m * cbn + (c - c0))
-                          : reinterpret_cast<uint4*>(O + (size_t)m * p.out_ld + p.out_off + c);
-        *dst = __builtin_bit_cast(uint4, o);
+        if constexpr (ALLF) {
+          const unsigned off = (unsigned)((((long)rr * p.wo + col) * cbn + 8 * g) * 2);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, o), zs, ok ? off : OOB, 0, 0);
+        } else {
+          const long m = m0 + (long)rr * p.wo + col;
+          uint4* dst = !ok ? h_sink + lane
+                       : fz ? reinterpret_cast<uint4*>(Z + (size_t)m * cbn + (c - c0))
+                            : reinterpret_cast<uint4*>(O + (size_t)m * p.out_ld + p.out_off + c);
+          *dst = __builtin_bit_cast(uint4, o);
+        }
       }
     }
     zero_acc();
@@ -718,7 +730,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       if constexpr (ES == 4) load_r(q);
       const int qr = ES == 2 ? q : 0;
       const int cl = 32 * q + 8 * g, c = n0 + cl;
-      const bool fz = c >= c0 && c < c1;
+      const bool fz = ALLF || (c >= c0 && c < c1);
+      const __amdgpu_buffer_rsrc_t zs = dma::brsrc(ALLF ? (const void*)(Z + m0 * cbn + n0 + 32 * q) : (const void*)Z);
       float ca[8], cb[8], ce[8];
       lds8(par + cl, ca);
       lds8(par + BN + cl, cb);
@@ -756,7 +769,17 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           }
         }
         TE* dp = fz ? Z + (size_t)m * cbn + (c - c0) : O + (size_t)m * p.out_ld + p.out_off + c;
-        if constexpr (ES == 2) {
+        if constexpr (ALLF) {  // as in epilogue_bnb16
+          const unsigned off = (unsigned)((((long)rr * p.wo + col) * cbn + 8 * g) * ES);
+          if constexpr (ES == 2) {
+            __builtin_amdgcn_raw_buffer_store_b128(pack8(v), zs, ok ? off : OOB, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, f32x4{v[0], v[1], v[2], v[3]}), zs,
+                                                   ok ? off : OOB, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, f32x4{v[4], v[5], v[6], v[7]}), zs,
+                                                   ok ? off + 16 : OOB, 0, 0);
+          }
+        } else if constexpr (ES == 2) {
           uint4* dst = !ok ? h_sink + lane : reinterpret_cast<uint4*>(dp);
           *dst = __builtin_bit_cast(uint4, pack8(v));
         } else {
@@ -1000,11 +1023,17 @@ bool halo_plan(const FwdArgs& a, HaloPlan& pl, bool f32 = false) {
 template <typename T, int BN, int EPI>
 void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
   if constexpr (EPI == 2) {
-    if (h.f.pool_out) {  // the routed pooled gradient (cnnitmo_conv3x3_dgrad_bn_pooled; 32-column blocks, halo_plan)
+    if (h.f.pool_out) {  // the routed pooled gradient (cnnitmo_conv3x3_dgrad_bn_pooled; 32-column blocks,
+                         // every column fused: halo_plan)
       if constexpr (BN == 32) {
-        if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true>), dim3(grid), dim3(NT), 0, s, h);
-        else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true>), dim3(grid), dim3(NT), 0, s, h);
+        if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, true, 16, true>), dim3(grid), dim3(NT), 0, s, h);
+        else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, true, 16, true>), dim3(grid), dim3(NT), 0, s, h);
       }
+      return;
+    }
+    if (h.f.bnb_c0 == 0 && h.f.bnb_c1 == h.f.N) {  // ALLF
+      if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, false, 16, true>), dim3(grid), dim3(NT), 0, s, h);
+      else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, false, 16, true>), dim3(grid), dim3(NT), 0, s, h);
       return;
     }
   }
