@@ -264,7 +264,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       for (int i = 0; i < NPI; ++i) {
         const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
         const bool ok = (unsigned)yy < (unsigned)p.hs && (unsigned)xx < (unsigned)p.ws;
-        pvo[i] = ok ? ((pkey[i] >> 2) * (unsigned)ld + (pkey[i] & 3) * PE) * ES : OOB;
+        // (any offset with the top bit set is out of range: OR-ing it in keeps this branch-free)
+        pvo[i] = ((pkey[i] >> 2) * (unsigned)ld + (pkey[i] & 3) * PE) * ES | (ok ? 0u : OOB);
       }
     } else {
       pbase = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + c) * ES);
@@ -508,9 +509,32 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
         if constexpr (EPI == 1 || EPI == 3) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) v[k] += bj[k];
-          if (bt && (oh == 0 || oh == p.ho - 1 || ow == 0 || ow == p.wo - 1)) {
+          if (bt && (oh == 0 || oh == p.ho - 1 || ow == 0 || ow == p.wo - 1) && POOL && !RES) {
+            // (the pooled non-resident kernel keeps the branching form: the branch-free one pushes
+            // its fragment-address table into scratch inside the K loop)
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] -= border_corr(utb + (cl + k) * 8, oh, ow, p.ho, p.wo);
+          } else if (bt && (oh == 0 || oh == p.ho - 1 || ow == 0 || ow == p.wo - 1)) {
+            // border_corr (igemm_common.h) without its per-lane branches (each an exec-mask branch
+            // around an LDS load): the same terms in the same order, absent ones as exact zeros
+            const float t = oh == 0 ? 1.f : 0.f, b = oh == p.ho - 1 ? 1.f : 0.f;
+            const float l = ow == 0 ? 1.f : 0.f, r = ow == p.wo - 1 ? 1.f : 0.f;
+            const float tl = t * l, tr = t * r, bl = b * l, br = b * r;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float4 u0 = *reinterpret_cast<const float4*>(utb + (cl + k) * 8);
+              const float4 u1 = *reinterpret_cast<const float4*>(utb + (cl + k) * 8 + 4);
+              float c = 0.f;
+              c = fmaf(t, u0.x, c);
+              c = fmaf(b, u0.y, c);
+              c = fmaf(l, u0.z, c);
+              c = fmaf(r, u0.w, c);
+              c = fmaf(-tl, u1.x, c);
+              c = fmaf(-tr, u1.y, c);
+              c = fmaf(-bl, u1.z, c);
+              c = fmaf(-br, u1.w, c);
+              v[k] -= c;
+            }
           }
           if (relu) {
 #pragma unroll

@@ -14,9 +14,10 @@ typedef int i32x2 __attribute__((ext_vector_type(2)));
 // voffset at or beyond num_records: a load lands zeros, a store is dropped
 constexpr unsigned OOB = 0x80000000u;
 
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
-}
+// LDS address of a generic pointer into LDS: the low 32 bits of a flat address in the shared
+// aperture are the LDS offset.  (The address-space cast also maps a null pointer, a compare and
+// two selects per call: about five scalar instructions per LDS-DMA piece.)
+__device__ __forceinline__ unsigned lds_addr(const void* p) { return (unsigned)(uintptr_t)p; }
 
 // raw buffer descriptor over [base, base + 2 GB) from a wave-uniform address
 __device__ __forceinline__ i32x4 rsrc(uintptr_t base) {
