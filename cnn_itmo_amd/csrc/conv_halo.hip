@@ -663,7 +663,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     // after the ring's pieces.  Non-temporal r loads and epilogue stores (to keep the patch
     // lines in L2 for the next chunk) measured 1-4 % slower on levels 0-2.)
     if constexpr (EARLY) {
-      dma::wait_vm_dyn(npost);  // the early loads, not the npost younger DMA pieces
+      dma::wait_vm_ge<L>(npost);  // the early loads, not the npost (0 or L) younger DMA pieces
     } else {
       load_r16(e);
       dma::wait_vm<0>();
@@ -853,7 +853,11 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   mq[ST - 1] = issued;
   int buf = 0;
   for (long t = 0; t < T; ++t) {
-    dma::wait_vm_dyn(issued - mq[0]);
+    // younger than this item's pieces: the previous tile's epilogue stores (NST) or nothing.
+    // (The generic fused dgrad, dec6's, keeps the switch: with the two-way wait its register
+    // allocation reloads fragment addresses from scratch inside the K loop.)
+    if constexpr (EPI == 2 && !ALLF) dma::wait_vm_dyn(issued - mq[0]);
+    else dma::wait_vm_ge<NST>(issued - mq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);

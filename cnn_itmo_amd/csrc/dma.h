@@ -58,6 +58,15 @@ __device__ __forceinline__ void lds16s(unsigned voff, i32x4 rs, unsigned soff, u
 template <int N> __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
+// Wait until at most n vector-memory operations are outstanding, for a call site whose n is
+// A or 0 (anything else waits for A if n >= A, for all otherwise: never less than asked).  Two
+// uniform branches instead of wait_vm_dyn's 48-way switch, which the structurizer turns into
+// a chain of flag tests (tens of scalar instructions per wait).
+template <int A> __device__ __forceinline__ void wait_vm_ge(int n) {
+  if (n >= A) wait_vm<A>();
+  else wait_vm<0>();
+}
+
 // s_waitcnt takes an immediate: dispatch a wave-uniform count (0..47; larger waits for all)
 __device__ __forceinline__ void wait_vm_dyn(int n) {
   switch (n) {
