@@ -80,4 +80,14 @@ __device__ __forceinline__ void wait_vm_dyn(int n) {
   }
 }
 
+// Exact wait for a count that is usually small: counts 0..3 go through a short chain of uniform
+// branches, others through wait_vm_dyn.
+__device__ __forceinline__ void wait_vm_small(int n) {
+  if (n <= 0) wait_vm<0>();
+  else if (n == 1) wait_vm<1>();
+  else if (n == 2) wait_vm<2>();
+  else if (n == 3) wait_vm<3>();
+  else wait_vm_dyn(n);
+}
+
 }  // namespace dma

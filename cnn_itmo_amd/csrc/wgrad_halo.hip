@@ -268,7 +268,7 @@ __global__ __launch_bounds__(3 * WM * WN * 64) void wgrad_halo_kernel(const WHAr
   };
   for (int k = 0; k < nrows; k += R) {
     const int last = nrows - k < R ? nrows - k - 1 : R - 1;  // rows k .. k+last this step
-    dma::wait_vm_dyn(issued - gq[last]);
+    dma::wait_vm_small(issued - gq[last]);  // (0 in steady state when D == R, one group when D == R + 1)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -459,7 +459,7 @@ __global__ __launch_bounds__(3 * (BM / 32) * wf_wn(BN) * 64) void wgrad_halo_f32
   int y = (int)(g0 % p.H);
   auto nxt = [](int sl, int n) { return sl + 1 == n ? 0 : sl + 1; };
   for (int k = 0; k < nrows; ++k) {
-    dma::wait_vm_dyn(issued - gq[0]);
+    dma::wait_vm_small(issued - gq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
