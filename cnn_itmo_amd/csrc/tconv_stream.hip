@@ -385,7 +385,10 @@ __global__ __launch_bounds__(512) void tconv_stream_kernel(const TSArgs p) {
   It cur;  // the item being computed
   it_init(cur);
   for (long q = 0; q < T; ++q) {
-    dma::wait_vm_dyn(issued - mq[0]);
+    // younger than this item's pieces: the next ST - 2 items' two pieces each, plus around a
+    // tile's end its r pieces and epilogue stores; waiting down to 2 (ST - 2) then also retires
+    // those r pieces, issued an item or more ago (a two-way wait instead of the switch)
+    dma::wait_vm_ge<2 * (ST - 2)>(issued - mq[0]);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
