@@ -249,17 +249,24 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
   uintptr_t pbase = 0, bbase = 0;
   char* iPs = smem;
   unsigned pvo[NPI];
+  // the tile's patch origin in each source (64-bit products), recomputed at its first chunk only;
+  // a chunk then adds its channel offset
+  uintptr_t tb1 = 0, tb2 = 0;
+  const uintptr_t wb0 = (uintptr_t)(Wt + (size_t)n0 * K);
   auto issue_prep = [&](int buf) {
     const Pos& s = ip;
     iPs = smem + buf * STAGE;
-    const long po = ((long)s.img * p.hs + s.y0 - 1) * p.ws + s.x0 - 1;  // patch origin pixel (may be < 0)
     const int c = s.ch * CC;
-    bbase = (uintptr_t)(Wt + (size_t)n0 * K + c);
+    if (s.ch == 0) {
+      const long po = ((long)s.img * p.hs + s.y0 - 1) * p.ws + s.x0 - 1;  // patch origin pixel (may be < 0)
+      tb1 = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off) * ES);
+      if constexpr (EPI == 1) tb2 = (uintptr_t)X2 + (uintptr_t)((po * p.a2_ld + p.a2_off - cin1) * ES);
+    }
+    bbase = wb0 + (uintptr_t)(c * ES);
     if constexpr (EPI == 1) {
       const bool second = c >= cin1;
       const long ld = second ? p.a2_ld : p.a_ld;
-      pbase = second ? (uintptr_t)X2 + (uintptr_t)((po * ld + p.a2_off + c - cin1) * ES)
-                     : (uintptr_t)X + (uintptr_t)((po * ld + p.a_off + c) * ES);
+      pbase = (second ? tb2 : tb1) + (uintptr_t)(c * ES);
 #pragma unroll
       for (int i = 0; i < NPI; ++i) {
         const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
@@ -268,7 +275,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
         pvo[i] = ((pkey[i] >> 2) * (unsigned)ld + (pkey[i] & 3) * PE) * ES | (ok ? 0u : OOB);
       }
     } else {
-      pbase = (uintptr_t)X + (uintptr_t)((po * p.a_ld + p.a_off + c) * ES);
+      pbase = tb1 + (uintptr_t)(c * ES);
 #pragma unroll
       for (int i = 0; i < NPI; ++i) {
         const int yy = s.y0 + ppy[i], xx = s.x0 + ppx[i];
