@@ -467,7 +467,10 @@ __global__ __launch_bounds__(WM * WN * 64) void igemm_fwd2p_kernel(const FwdArgs
 // workgroups of a row block run side by side and share its x rows in L2).  Stats rows:
 // one per (XCD, slot / nblocks, wave row), every (row, column) written exactly once (a
 // workgroup without tiles writes zeros).
-template <int BM, int BN, int WM, int WN>
+// TRAIN: the training flags (ReLU + BN sums, no affine) as constants: with runtime flags the
+// compiler computes both sides of each flag test per value and selects (two selects and an FMA
+// per value that the training step never needs).
+template <int BM, int BN, int WM, int WN, bool TRAIN = false>
 __global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs p) {
   using C = Fwd2Cfg<bf16, BM, BN, WM, WN, 2>;
   constexpr int VE = C::VE, KE = C::KE, TM = C::TM, TN = C::TN, FM = C::FM, FN = C::FN;
@@ -492,7 +495,8 @@ __global__ __launch_bounds__(WM * WN * 64) void tconv_fwd2p_kernel(const FwdArgs
   const bf16* __restrict__ A = (const bf16*)p.a;
   const bf16* __restrict__ B = (const bf16*)p.b;
   const unsigned hw32 = (unsigned)((long)p.ho * p.wo), wo32 = (unsigned)p.wo;
-  const bool relu = p.flags & CNNITMO_RELU, stats = p.flags & CNNITMO_STATS, aff = p.flags & CNNITMO_AFFINE;
+  const bool relu = TRAIN || (p.flags & CNNITMO_RELU), stats = TRAIN || (p.flags & CNNITMO_STATS);
+  const bool aff = !TRAIN && (p.flags & CNNITMO_AFFINE);
   for (int i = tid; i < BN; i += WM * WN * 64) {
     const int n = n0 + i, co = n - (n / p.cout) * p.cout;
     bias_s[i] = !p.bias ? 0.f : p.bias[(p.flags & CNNITMO_BIAS_PER_COL) ? n : co];
@@ -753,7 +757,11 @@ int launch_tfwd2p(FwdArgs a, hipStream_t s, const char* what) {
   a.mblocks = (int)((a.M + 255) / 256);
   a.nblocks = a.N / 256;
   const int g = 8 * std::max(cu_count() / 8, 1);
-  hipLaunchKernelGGL((tconv_fwd2p_kernel<256, 256, 2, 4>), dim3((unsigned)g), dim3(512), 0, s, a);
+  const int fl = a.flags & ~CNNITMO_BIAS_PER_COL;
+  if (fl == (CNNITMO_RELU | CNNITMO_STATS))
+    hipLaunchKernelGGL((tconv_fwd2p_kernel<256, 256, 2, 4, true>), dim3((unsigned)g), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((tconv_fwd2p_kernel<256, 256, 2, 4>), dim3((unsigned)g), dim3(512), 0, s, a);
   return cnnitmo_check_launch(what);
 }
 
