@@ -43,6 +43,7 @@
 // g (as cnnitmo_bn_bwd_apply computes it) plus sums of dz by pixel parity; the
 // other columns are stored as g.
 #include <cstdio>
+#include <type_traits>
 
 #include "dma.h"
 #include "igemm_common.h"
@@ -122,8 +123,9 @@ struct HaloArgs {
 // (pool_sign), and the pooled value is itself a folded value.  Inference stores y (AFFINE)
 // and pools it by its maximum.
 // ALT, EPI 1 (NOSUM): no BN partial sums (the inference forward): the 2 x FP x 8 accumulators live
-// across the whole launch otherwise.  ALT, EPI 2 (ALLF): every column is BN-fused (c0 = 0, c1 = N:
-// every fused dgrad of the model but dec6's): the epilogue has no per-column branch.  A per-lane
+// across the whole launch otherwise.  ALT, EPI 2 (ALLF): every column is BN-fused (c0 = 0, c1 = N),
+// or (bf16, streamed weights) c0 is a multiple of BN and c1 = N, so that a column block is fused or
+// plain as a whole (dec6's [skip 256 | up 512]): the epilogue has no per-column branch.  A per-lane
 // `fused` test in the value loop compiles to an exec-mask branch per value (about ten scalar
 // instructions each, 91 such branches per epilogue); the ALLF epilogue stores through raw-buffer
 // offsets from the wave's first pixel.
@@ -187,7 +189,8 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
     const int cbn = p.bnb_c1 - p.bnb_c0;
     for (int i = tid; i < 3 * BN; i += NT) {
       const int k = i / BN, c = n0 + i % BN;
-      par[i] = (c >= p.bnb_c0 && c < p.bnb_c1) ? p.bnb_coef[k * cbn + c - p.bnb_c0] : 0.f;
+      // (ALLF: a plain column gets a = 1, b = e = 0, so the fused expression stores g itself)
+      par[i] = (c >= p.bnb_c0 && c < p.bnb_c1) ? p.bnb_coef[k * cbn + c - p.bnb_c0] : (ALLF && k == 0 ? 1.f : 0.f);
     }
   }
 
@@ -685,8 +688,16 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
       lds8(par + cl, ca);
       lds8(par + BN + cl, cb);
       lds8(par + 2 * BN + cl, ce);
-      // ALLF: dz of the pair's columns at the wave's first pixel (c0 = 0, cbn = N)
-      const __amdgpu_buffer_rsrc_t zs = dma::brsrc(ALLF ? (const void*)(Z + m0 * cbn + n0 + 32 * q) : (const void*)Z);
+      // ALLF: the pair's columns at the wave's first pixel, in dz (a fused block) or in the plain
+      // gradient's view (a block below c0, whose r reads as 0: the ReLU test then compares with -1)
+      // (the resident-weight and routed kernels take c0 = 0 only: launch_cfg)
+      const bool bfz = !ALLF || RES || POOL || n0 >= c0;
+      const __amdgpu_buffer_rsrc_t zs =
+          dma::brsrc(!ALLF ? (const void*)Z
+                           : bfz ? (const void*)(Z + m0 * cbn + (n0 - c0) + 32 * q)
+                                 : (const void*)(O + m0 * p.out_ld + p.out_off + n0 + 32 * q));
+      const long zld = bfz ? (long)cbn : p.out_ld;
+      const float rmin = bfz ? 0.f : -1.f;
 #pragma unroll
       for (int f = 0; f < FM; ++f) {
         const int rr = f / FMR, col = (f % FMR) * 16 + pxl;
@@ -706,7 +717,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
             // sums take no `ok` select.  This holds because rv comes from load_r16's raw-buffer loads
             // at r_off, which is OOB (the load returns 0) for every out-of-image or out-of-range
             // piece; the fp32 twin, epilogue_bnb32, keeps the select.)
-            o[k] = from_f32<bf16>(r > 0.f ? ca[k] * gk - cb[k] * r + ce[k] : 0.f);
+            o[k] = from_f32<bf16>(r > rmin ? ca[k] * gk - cb[k] * r + ce[k] : 0.f);
             if (rr == 0) sa[q][k] += to_f32(o[k]);
             else sb[q][k] += to_f32(o[k]);
           } else {
@@ -714,7 +725,7 @@ __global__ __launch_bounds__(NT) void halo_conv_kernel(const HaloArgs h) {
           }
         }
         if constexpr (ALLF) {
-          const unsigned off = (unsigned)((((long)rr * p.wo + col) * cbn + 8 * g) * 2);
+          const unsigned off = (unsigned)((((long)rr * p.wo + col) * zld + 8 * g) * 2);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(dma::i32x4, o), zs, ok ? off : OOB, 0, 0);
         } else {
           const long m = m0 + (long)rr * p.wo + col;
@@ -1066,7 +1077,10 @@ void launch_cfg(const HaloArgs& h, bool res, int grid, hipStream_t s) {
       }
       return;
     }
-    if (h.f.bnb_c0 == 0 && h.f.bnb_c1 == h.f.N) {  // ALLF
+    // ALLF: every column fused, or (bf16) every block either fused or plain
+    const bool allf = h.f.bnb_c1 == h.f.N &&
+                      (h.f.bnb_c0 == 0 || (std::is_same<T, bf16>::value && !res && h.f.bnb_c0 % BN == 0));
+    if (allf) {
       if (res) hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, true, false, 16, true>), dim3(grid), dim3(NT), 0, s, h);
       else hipLaunchKernelGGL((halo_conv_kernel<T, BN, EPI, false, false, 16, true>), dim3(grid), dim3(NT), 0, s, h);
       return;
